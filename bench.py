@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: GGNN propagation fwd+bwd, instances/sec (graphs/s).
+
+Metric and config from BASELINE.json: hidden=256, v=128, e=4 edge types
+(C = 2e = 8 adjacency channels), T=5, batch 256 graphs per GPU (configs[2]).
+One "step" = one pass of the hot path over one batch already resident in HBM:
+  pack weights (fp32 -> bf16 fragments) + stage adjacency ([b,C,v,v] fp32 ->
+  bf16 + transpose) + T-step forward + full backward (dL/dh0 and all six
+  weight gradients) [+ one RCCL all-reduce of the flat gradient buffer when
+  N > 1].
+Weak scaling: every rank owns its own 256-graph batch; value = N*256 / t_step
+with t_step the max over ranks.
+
+Run:  python bench.py [--gpus N] [--steps K] [--warmup W]
+      (N > 1 under torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CFG = dict(b=256, v=128, h=256, e=4, T=5)
+BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_graph(v, h, C, T):
+    """Algorithmic FLOPs per graph."""
+    mt = 2 * v * h * h * C
+    agg = 2 * v * v * C * h
+    gru = 12 * v * h * h
+    return dict(mt=mt, agg=agg, gru=gru, fwd=T * (mt + agg + gru), total=T * (2 * agg + 3 * mt + 3 * gru))
+
+
+def kernel_algo_flops(kind, b, v, h, C, T):
+    """Algorithmic FLOPs of ONE launch of a kernel kind at this config."""
+    f = flops_per_graph(v, h, C, T)
+    if kind in ("prop_fwd", "prop_bwd"):
+        return b * (f["mt"] + f["agg"])
+    if kind in ("gru_fwd", "gru_bwd"):
+        return b * f["gru"]
+    if kind == "wgrad":   # dW (MT-sized) + dWg, dWc (GRU-sized) over all T steps
+        return T * b * (f["mt"] + f["gru"])
+    return 0
+
+
+def cpu_baseline(seconds=10.0, sample_b=8):
+    """The oracle (numpy fp32 + OpenBLAS restatement of the reference math) on
+    the host: forward + explicit backward of the same config on `sample_b`
+    graphs, repeated for ~`seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ggnn_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    C = 2 * CFG["e"]
+    A, h0 = O.synthetic_batch(sample_b, CFG["v"], CFG["h"], C, seed=1)
+    w = O.synthetic_weights(CFG["h"], C, seed=1, parity_bias=False)
+    dhT = np.ones_like(h0)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    try:
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            hT, caches = O.forward(A, h0, w, CFG["T"])
+            O.backward(A, dhT, caches, w)
+            n += sample_b
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        if ctx is not None:
+            ctx.unregister() if hasattr(ctx, "unregister") else None
+    return dict(value=n / el, unit="graphs/s", cores=cores, kind="port",
+                sample="oracle fp32 numpy fwd+bwd, %d graphs/batch (v=%d h=%d C=%d T=%d), %d graphs in %.1f s"
+                       % (sample_b, CFG["v"], CFG["h"], C, CFG["T"], n, el))
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        try:
+            with open(p) as f:
+                return json.load(f)
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as tdist
+    from ggnn_amd.dist import FlatGradients, init_from_env
+    from ggnn_amd.engine import PropagationEngine
+    from ggnn_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ggnn_oracle as O  # synthetic input generator; not timed
+
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    b, v, h, T = CFG["b"], CFG["v"], CFG["h"], CFG["T"]
+    C = 2 * CFG["e"]
+    A, h0 = O.synthetic_batch(b, v, h, C, seed=1 + 1000 * rank)
+    w = O.synthetic_weights(h, C, seed=1)
+    A_d = torch.from_numpy(A).to(dev)
+    h0_d = torch.from_numpy(h0).to(dev)
+    w_d = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
+    dhT = torch.from_numpy(np.random.default_rng(7 + rank).standard_normal((b, v, h)).astype(np.float32)).to(dev)
+    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev)
+    grads = FlatGradients(h, C, True, device=dev)
+    gviews = dict(grads.views)
+    gviews["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+    out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+
+    def step():
+        pack = eng.pack_weights(w_d)
+        eng.set_adjacency(A_d)
+        eng.forward(h0_d, pack, T, training=True, out=out)
+        eng.backward(dhT, gviews)
+        grads.all_reduce()
+
+    def barrier():
+        if world > 1:
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    timer = _lib.KernelTimer(max_launches=200 * max(args.steps, 1))
+    with timer:
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        barrier()
+        t1 = time.perf_counter()
+    dt = (t1 - t0) / args.steps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    # roofline of the dominant kernel (largest total time in the timed region)
+    kinds = {k: ms for k, ms in timer.total_ms.items() if timer.launches.get(k)}
+    dom = max(kinds, key=kinds.get)
+    n_l = timer.launches[dom]
+    avg_ms = timer.total_ms[dom] / n_l
+    fl = kernel_algo_flops(dom, b, v, h, C, T)
+    achieved = fl / (avg_ms * 1e-3) / 1e12 if fl else None
+    traffic = None
+    tr = load_traffic()
+    if tr and tr.get("kernel") == dom:
+        traffic = tr.get("hbm_bytes_per_launch")
+    roof = {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": (achieved / BF16_DENSE_PEAK_TFLOPS) if achieved else None,
+            "traffic": traffic, "avg_launch_ms": avg_ms, "algo_flops_per_launch": fl}
+    breakdown = {k: {"ms_per_step": timer.total_ms[k] / args.steps, "launches_per_step": timer.launches[k] / args.steps}
+                 for k in kinds}
+
+    if rank == 0:
+        fpg = flops_per_graph(v, h, C, T)["total"]
+        value = world * b / dt
+        res = {
+            "metric": "instances/sec (graphs/s) GGNN fwd+bwd, hidden=256 v=128 e=4 T=5",
+            "value": value,
+            "unit": "graphs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (SURVEY §8d generator: Bernoulli(0.1) adjacency on n~U{v/2..v} active nodes, glorot weights)",
+            "config": {"workload": "configs[2]: b=256 graphs/GPU, v=128, hidden=256, e=4 (C=8), T=5, fwd+bwd",
+                       "global_batch": world * b, "parallelism": "dp%d" % world},
+            "roofline": roof,
+            "achieved_step_tflops": world * b * fpg / dt / 1e12,
+            "kernel_breakdown": breakdown,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+"""ctypes binding of ``libggnn.so`` (the C ABI declared in ``include/ggnn.h``).
+
+The product path has exactly one implementation: the HIP kernels behind this
+library.  If the library is missing or fails to load, every entry point
+raises -- there is no CPU or PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from .build import LIB
+
+GGNN_USE_EDGE_BIAS = 1
+
+# Every symbol include/ggnn.h declares (checked by tests/test_lib.py).
+EXPORTED = (
+    "ggnn_version", "ggnn_last_error", "ggnn_check_dims", "ggnn_workspace_bytes",
+    "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
+    "ggnn_forward", "ggnn_backward", "ggnn_kernel_kind_name", "ggnn_profile_begin",
+    "ggnn_profile_end",
+)
+NUM_KERNEL_KINDS = 8
+
+
+class GGNNDims(ctypes.Structure):
+    _fields_ = [("b", ctypes.c_int32), ("v", ctypes.c_int32), ("h", ctypes.c_int32),
+                ("C", ctypes.c_int32), ("T", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+    def __repr__(self):
+        return "GGNNDims(b=%d, v=%d, h=%d, C=%d, T=%d, flags=%d)" % (
+            self.b, self.v, self.h, self.C, self.T, self.flags)
+
+
+class GGNNError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_DP = ctypes.POINTER(GGNNDims)
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libggnn.so (once).  Raises GGNNError if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = path or os.environ.get("GGNN_LIB", LIB)
+        if not os.path.exists(path):
+            raise GGNNError("libggnn.so not found at %s: run `python -m ggnn_amd.build` "
+                            "(or __graft_entry__.build()) first" % path)
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        lib.ggnn_version.restype = _I
+        lib.ggnn_version.argtypes = []
+        lib.ggnn_last_error.restype = ctypes.c_char_p
+        lib.ggnn_last_error.argtypes = []
+        lib.ggnn_check_dims.restype = _I
+        lib.ggnn_check_dims.argtypes = [_DP]
+        lib.ggnn_workspace_bytes.restype = _I
+        lib.ggnn_workspace_bytes.argtypes = [_DP, _I, ctypes.POINTER(ctypes.c_size_t)]
+        lib.ggnn_adjacency_bytes.restype = _I
+        lib.ggnn_adjacency_bytes.argtypes = [_DP, ctypes.POINTER(ctypes.c_size_t)]
+        lib.ggnn_weight_pack_bytes.restype = _I
+        lib.ggnn_weight_pack_bytes.argtypes = [_DP, ctypes.POINTER(ctypes.c_size_t)]
+        lib.ggnn_pack_weights.restype = _I
+        lib.ggnn_pack_weights.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P]
+        lib.ggnn_set_adjacency.restype = _I
+        lib.ggnn_set_adjacency.argtypes = [_DP, _P, _P, _P]
+        lib.ggnn_forward.restype = _I
+        lib.ggnn_forward.argtypes = [_DP, _P, _P, _P, _I, _P, _P, _P]
+        lib.ggnn_backward.restype = _I
+        lib.ggnn_backward.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+        lib.ggnn_kernel_kind_name.restype = ctypes.c_char_p
+        lib.ggnn_kernel_kind_name.argtypes = [_I]
+        lib.ggnn_profile_begin.restype = _I
+        lib.ggnn_profile_begin.argtypes = [_I]
+        lib.ggnn_profile_end.restype = _I
+        lib.ggnn_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().ggnn_last_error().decode(errors="replace")
+        raise GGNNError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True) -> GGNNDims:
+    return GGNNDims(int(b), int(v), int(h), int(C), int(T), GGNN_USE_EDGE_BIAS if use_edge_bias else 0)
+
+
+def check_dims(d: GGNNDims) -> None:
+    check(load().ggnn_check_dims(ctypes.byref(d)), "ggnn_check_dims(%r)" % (d,))
+
+
+def workspace_bytes(d: GGNNDims, training: bool) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().ggnn_workspace_bytes(ctypes.byref(d), int(bool(training)), ctypes.byref(n)),
+          "ggnn_workspace_bytes")
+    return int(n.value)
+
+
+def adjacency_bytes(d: GGNNDims) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().ggnn_adjacency_bytes(ctypes.byref(d), ctypes.byref(n)), "ggnn_adjacency_bytes")
+    return int(n.value)
+
+
+def weight_pack_bytes(d: GGNNDims) -> int:
+    n = ctypes.c_size_t(0)
+    check(load().ggnn_weight_pack_bytes(ctypes.byref(d), ctypes.byref(n)), "ggnn_weight_pack_bytes")
+    return int(n.value)
+
+
+class KernelTimer:
+    """Context manager: HIP-event time of every libggnn launch, per kernel kind."""
+
+    def __init__(self, max_launches: int = 100000):
+        self.max_launches = max_launches
+        self.total_ms = {}
+        self.launches = {}
+
+    def __enter__(self):
+        check(load().ggnn_profile_begin(self.max_launches), "ggnn_profile_begin")
+        return self
+
+    def __exit__(self, *exc):
+        ms = (ctypes.c_double * NUM_KERNEL_KINDS)()
+        n = (ctypes.c_int * NUM_KERNEL_KINDS)()
+        check(load().ggnn_profile_end(ms, n), "ggnn_profile_end")
+        for k in range(NUM_KERNEL_KINDS):
+            name = load().ggnn_kernel_kind_name(k).decode()
+            self.total_ms[name] = ms[k]
+            self.launches[name] = n[k]
+        return False

@@ -1,0 +1,82 @@
+"""Data-parallel plumbing: one process per GPU, gradients all-reduced over RCCL.
+
+The propagation path shards naturally by graph (chem_tensorflow_dense.py:414-428
+contracts only inside graph g); the only cross-graph coupling is the batch sum
+of the weight gradients (TF autodiff, chem_tensorflow.py:496).  Each rank runs
+its own batch through the engine, then ONE all-reduce of a flat fp32 gradient
+buffer per step (3.68 MB at h=256, C=8) sums them.  The per-tensor
+clip_by_norm of the reference (chem_tensorflow.py:498-503) must see the
+reduced gradient, so it runs after this reduction (optimizer, next row).
+
+``torch.distributed`` with backend "nccl" is RCCL on ROCm; "gloo" is used by
+the CPU tests.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as tdist
+
+GRAD_ORDER = ("edge_weights", "edge_biases", "gates_kernel", "gates_bias",
+              "candidate_kernel", "candidate_bias")
+
+
+def grad_shapes(hidden: int, channels: int, use_edge_bias: bool = True):
+    h, C = hidden, channels
+    shapes = {
+        "edge_weights": (C, h, h),
+        "edge_biases": (C, 1, h),
+        "gates_kernel": (2 * h, 2 * h),
+        "gates_bias": (2 * h,),
+        "candidate_kernel": (2 * h, h),
+        "candidate_bias": (h,),
+    }
+    if not use_edge_bias:
+        shapes.pop("edge_biases")
+    return shapes
+
+
+class FlatGradients:
+    """One contiguous fp32 buffer holding every weight gradient of the path;
+    ``views`` are the per-tensor views the engine writes into, so the
+    all-reduce is a single collective with no packing copy."""
+
+    def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None):
+        self.shapes = grad_shapes(hidden, channels, use_edge_bias)
+        total = sum(int(torch.Size(s).numel()) for s in self.shapes.values())
+        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+        self.views = {}
+        off = 0
+        for name in GRAD_ORDER:
+            if name not in self.shapes:
+                continue
+            n = int(torch.Size(self.shapes[name]).numel())
+            self.views[name] = self.flat[off:off + n].view(self.shapes[name])
+            off += n
+
+    @property
+    def nbytes(self) -> int:
+        return self.flat.numel() * 4
+
+    def all_reduce(self, group=None) -> None:
+        """Sum the gradients over all ranks (RCCL on GPUs, gloo on CPU)."""
+        if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size(group) > 1:
+            tdist.all_reduce(self.flat, op=tdist.ReduceOp.SUM, group=group)
+
+
+def init_from_env(backend: str | None = None):
+    """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local_rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not tdist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            tdist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
+    return rank, world, local

@@ -1,0 +1,173 @@
+"""Host-side driver of the HIP propagation engine.
+
+``PropagationEngine`` owns the device buffers of one batch shape and calls
+the C ABI (``include/ggnn.h``) on PyTorch's current HIP stream.  PyTorch is
+used only to hold device memory and to name the stream; every arithmetic op
+of the hot path runs in ``libggnn.so``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+WEIGHT_NAMES = ("edge_weights", "edge_biases", "gates_kernel", "gates_bias",
+                "candidate_kernel", "candidate_bias")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _require(t: torch.Tensor, shape, name: str):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor on the GPU, got %r" % (name, type(t)))
+    if t.device.type != "cuda":
+        raise ValueError("%s must live on a HIP device (got %s)" % (name, t.device))
+    if t.dtype != torch.float32:
+        raise TypeError("%s must be float32 (got %s)" % (name, t.dtype))
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError("%s: expected shape %s, got %s" % (name, tuple(shape), tuple(t.shape)))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+
+
+@dataclass
+class WeightPack:
+    """bf16 MFMA-fragment copy of one weight set (see ggnn_pack_weights)."""
+    buf: torch.Tensor
+    hidden: int
+    channels: int
+    use_edge_bias: bool
+
+
+class PropagationEngine:
+    """Runs ``compute_final_node_representations`` (chem_tensorflow_dense.py:312-340)
+    and its backward for batches of shape [b, C, v, v] / [b, v, h]."""
+
+    def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None):
+        self.h = int(hidden)
+        self.C = int(channels)
+        self.use_edge_bias = bool(use_edge_bias)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._lib = _lib.load()
+        self._adj = None            # staged adjacency buffer
+        self._batch = None          # (b, v) of the staged adjacency
+        self._ws = {}               # (b, v, T, training) -> workspace
+        self._trained = None        # (b, v, T, pack, ws) of the last training forward
+
+    # ------------------------------------------------------------------ utils
+    def dims(self, b: int, v: int, T: int) -> _lib.GGNNDims:
+        d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias)
+        _lib.check_dims(d)
+        return d
+
+    def workspace(self, b: int, v: int, T: int, training: bool) -> torch.Tensor:
+        key = (b, v, T, bool(training))
+        ws = self._ws.get(key)
+        if ws is None:
+            if len(self._ws) >= 4:      # keep a handful of shapes (bucketed batches)
+                self._ws.clear()
+            ws = torch.empty(_lib.workspace_bytes(self.dims(b, v, T), training),
+                             dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    # ---------------------------------------------------------------- weights
+    def pack_weights(self, weights: dict) -> WeightPack:
+        """weights: dict of fp32 device tensors with the reference's shapes:
+        edge_weights [C,h,h], edge_biases [C,1,h] (or [C,h]), gates_kernel [2h,2h],
+        gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h]."""
+        h, C = self.h, self.C
+        _require(weights["edge_weights"], (C, h, h), "edge_weights")
+        eb = weights.get("edge_biases") if self.use_edge_bias else None
+        if self.use_edge_bias:
+            if eb is None:
+                raise ValueError("use_edge_bias=True but no edge_biases given")
+            _require(eb, (C, 1, h) if eb.dim() == 3 else (C, h), "edge_biases")
+        _require(weights["gates_kernel"], (2 * h, 2 * h), "gates_kernel")
+        _require(weights["gates_bias"], (2 * h,), "gates_bias")
+        _require(weights["candidate_kernel"], (2 * h, h), "candidate_kernel")
+        _require(weights["candidate_bias"], (h,), "candidate_bias")
+        d = self.dims(1, 1, 1)
+        buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)
+        _lib.check(self._lib.ggnn_pack_weights(
+            ctypes.byref(d), _ptr(buf), _ptr(weights["edge_weights"]), _ptr(eb),
+            _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
+            _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream()),
+            "ggnn_pack_weights")
+        return WeightPack(buf, h, C, self.use_edge_bias)
+
+    # -------------------------------------------------------------- adjacency
+    def set_adjacency(self, adjacency: torch.Tensor) -> None:
+        """adjacency: [b, C, v, v] fp32 0/1 on the device (the reference's feed,
+        chem_tensorflow_dense.py:192-195)."""
+        if adjacency.dim() != 4 or adjacency.shape[1] != self.C or adjacency.shape[2] != adjacency.shape[3]:
+            raise ValueError("adjacency must be [b, %d, v, v], got %s" % (self.C, tuple(adjacency.shape)))
+        b, _, v, _ = adjacency.shape
+        _require(adjacency, (b, self.C, v, v), "adjacency")
+        d = self.dims(b, v, 1)
+        nbytes = _lib.adjacency_bytes(d)
+        if self._adj is None or self._adj.numel() < nbytes:
+            self._adj = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        _lib.check(self._lib.ggnn_set_adjacency(ctypes.byref(d), _ptr(self._adj), _ptr(adjacency), _stream()),
+                   "ggnn_set_adjacency")
+        self._batch = (int(b), int(v))
+        self._trained = None
+
+    @property
+    def batch_shape(self):
+        return self._batch
+
+    # ---------------------------------------------------------------- compute
+    def forward(self, h0: torch.Tensor, pack: WeightPack, T: int, training: bool = False,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+        if self._batch is None:
+            raise RuntimeError("set_adjacency() must be called before forward()")
+        b, v = self._batch
+        _require(h0, (b, v, self.h), "initial_node_representations")
+        ws = self.workspace(b, v, T, training)
+        d = self.dims(b, v, T)
+        if out is None:
+            out = torch.empty((b, v, self.h), dtype=torch.float32, device=self.device)
+        _require(out, (b, v, self.h), "out")
+        _lib.check(self._lib.ggnn_forward(ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws),
+                                          int(bool(training)), _ptr(h0), _ptr(out), _stream()), "ggnn_forward")
+        self._trained = (b, v, T, pack, ws) if training else None
+        return out
+
+    def alloc_grads(self, b: int, v: int) -> dict:
+        h, C, dev = self.h, self.C, self.device
+        return {
+            "h0": torch.empty((b, v, h), dtype=torch.float32, device=dev),
+            "edge_weights": torch.empty((C, h, h), dtype=torch.float32, device=dev),
+            "edge_biases": torch.empty((C, 1, h), dtype=torch.float32, device=dev) if self.use_edge_bias else None,
+            "gates_kernel": torch.empty((2 * h, 2 * h), dtype=torch.float32, device=dev),
+            "gates_bias": torch.empty((2 * h,), dtype=torch.float32, device=dev),
+            "candidate_kernel": torch.empty((2 * h, h), dtype=torch.float32, device=dev),
+            "candidate_bias": torch.empty((h,), dtype=torch.float32, device=dev),
+        }
+
+    def backward(self, dhT: torch.Tensor, grads: dict | None = None) -> dict:
+        """Backward of the last training forward.  Returns a dict with 'h0' and
+        the six weight gradients (reference shapes, fp32)."""
+        if self._trained is None:
+            raise RuntimeError("backward() needs a preceding forward(..., training=True) on this batch")
+        b, v, T, pack, ws = self._trained
+        _require(dhT, (b, v, self.h), "dL/dh_T")
+        if grads is None:
+            grads = self.alloc_grads(b, v)
+        d = self.dims(b, v, T)
+        _lib.check(self._lib.ggnn_backward(
+            ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws), _ptr(dhT), _ptr(grads["h0"]),
+            _ptr(grads["edge_weights"]), _ptr(grads.get("edge_biases")), _ptr(grads["gates_kernel"]),
+            _ptr(grads["gates_bias"]), _ptr(grads["candidate_kernel"]), _ptr(grads["candidate_bias"]),
+            _stream()), "ggnn_backward")
+        return grads

@@ -1,0 +1,127 @@
+/*
+ * ggnn.h -- C ABI of the MI355X-native GGNN propagation engine (libggnn.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *   DenseGGNNChemModel.compute_final_node_representations
+ *   (crismolav/ggnn, chem_tensorflow_dense.py:312-340, called from
+ *    chem_tensorflow.py:319-322)
+ * together with its TF-autodiff backward (chem_tensorflow.py:496).
+ *
+ * The reference has no FFI: the path is a Python template method that builds
+ * TensorFlow ops.  Each entry point below replaces one piece of that method:
+ *
+ *   ggnn_pack_weights   <- the path's variables, chem_tensorflow_dense.py:202-212
+ *                          (edge_weights [C,h,h], edge_biases [C,1,h]) and the
+ *                          GRUCell kernels/biases built at :237-241
+ *   ggnn_set_adjacency  <- the adjacency placeholder + transpose, :192-195
+ *                          (feed [b, C, v, v], row = receiving node, :65-83)
+ *   ggnn_forward        <- the T-step loop, :312-340 = compute_timestep_fast
+ *                          (:391-437) + GRUCell (:333), returns [b, v, h]
+ *   ggnn_backward       <- TF autodiff of the same loop (chem_tensorflow.py:496):
+ *                          dL/dh0 and the weight gradients (before clip/Adam)
+ *
+ * Conventions
+ *  - Every tensor argument is a raw device pointer (hipMalloc'd or any HIP
+ *    allocator, e.g. PyTorch-ROCm tensors used only as memory holders).
+ *  - Host-visible layouts are the reference's: row-major fp32,
+ *      adjacency [b][C][v][v] (0/1 values, row = receiver, col = sender),
+ *      h0 / hT / dhT / dh0 [b][v][h],
+ *      edge_weights [C][h][h] (in x out), edge_biases [C][h],
+ *      gates_kernel [2h][2h] (rows [x ; h], cols [r | u]), gates_bias [2h],
+ *      candidate_kernel [2h][h] (rows [x ; r*h]), candidate_bias [h].
+ *  - The caller owns all memory.  The library never allocates: it works
+ *    inside a caller-provided workspace sized by ggnn_workspace_bytes and a
+ *    weight pack sized by ggnn_weight_pack_bytes.
+ *  - All calls are asynchronous and stream-ordered on `stream`; they are safe
+ *    to capture into a hipGraph (no sync, no malloc inside).
+ *  - Return value: 0 on success, negative GGNN_E* on error; a description of
+ *    the last error of the calling thread is in ggnn_last_error().
+ *    No exception or abort crosses the ABI.
+ */
+#ifndef GGNN_H
+#define GGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* ggnn_stream_t; /* hipStream_t (0 = default stream) */
+
+enum {
+  GGNN_OK = 0,
+  GGNN_EINVAL = -1,    /* invalid dims / null pointer */
+  GGNN_EUNSUP = -2,    /* dims outside the compiled kernel set */
+  GGNN_ELAUNCH = -3,   /* HIP launch / runtime error */
+  GGNN_EALIGN = -4     /* pointer alignment */
+};
+
+/* flags */
+#define GGNN_USE_EDGE_BIAS 1 /* params['use_edge_bias'], chem_tensorflow_dense.py:158 */
+
+typedef struct ggnn_dims {
+  int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
+  int32_t v;     /* vertices per graph       (placeholders['num_vertices']) */
+  int32_t h;     /* hidden size              (params['hidden_size'])        */
+  int32_t C;     /* adjacency channels = 2 * num_edge_types                 */
+  int32_t T;     /* timesteps (params['num_timesteps'] or fixed_ts)         */
+  int32_t flags; /* GGNN_USE_EDGE_BIAS                                      */
+} ggnn_dims;
+
+int ggnn_version(void);
+const char* ggnn_last_error(void);
+
+/* Validate dims against the compiled kernel set: 1<=v<=128, h in {64,128,256},
+ * C>=1, T>=1, b>=1.  Returns 0 or GGNN_EUNSUP / GGNN_EINVAL. */
+int ggnn_check_dims(const ggnn_dims* d);
+
+/* Bytes of the per-batch workspace (activations saved for backward when
+ * training != 0), of one staged adjacency batch and of one weight pack. */
+int ggnn_workspace_bytes(const ggnn_dims* d, int training, size_t* bytes);
+int ggnn_adjacency_bytes(const ggnn_dims* d, size_t* bytes);
+int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes);
+
+/* Convert fp32 master weights into the engine's bf16 MFMA fragment layouts.
+ * edge_biases may be NULL when !(flags & GGNN_USE_EDGE_BIAS). */
+int ggnn_pack_weights(const ggnn_dims* d, void* pack,
+                      const float* edge_weights, const float* edge_biases,
+                      const float* gates_kernel, const float* gates_bias,
+                      const float* candidate_kernel, const float* candidate_bias,
+                      ggnn_stream_t stream);
+
+/* Stage one batch's adjacency [b][C][v][v] fp32 (0/1) into `adj` (sized by
+ * ggnn_adjacency_bytes): bf16 (exact for 0/1), its transpose and per-node
+ * in-degrees.  T and flags of d are ignored. */
+int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* adjacency,
+                       ggnn_stream_t stream);
+
+/* T-step forward.  h0, hT: [b][v][h] fp32.  training != 0 keeps what the
+ * backward needs inside ws (ws must have been sized with training != 0). */
+int ggnn_forward(const ggnn_dims* d, const void* pack, const void* adj, void* ws,
+                 int training, const float* h0, float* hT, ggnn_stream_t stream);
+
+/* Backward of the last training forward on ws (same d, pack, adj).
+ * dhT, dh0: [b][v][h] fp32.  Gradient outputs are OVERWRITTEN (not
+ * accumulated), fp32, reference layouts; d_edge_biases may be NULL when
+ * !(flags & GGNN_USE_EDGE_BIAS). */
+int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* ws,
+                  const float* dhT, float* dh0,
+                  float* d_edge_weights, float* d_edge_biases,
+                  float* d_gates_kernel, float* d_gates_bias,
+                  float* d_candidate_kernel, float* d_candidate_bias,
+                  ggnn_stream_t stream);
+
+/* Optional per-kernel timing (HIP events around every launch of the library
+ * on the launch's stream), used by bench.py for the roofline.  Not for use
+ * under graph capture.  total_ms / launches: arrays of GGNN_NUM_KERNEL_KINDS. */
+#define GGNN_NUM_KERNEL_KINDS 8
+const char* ggnn_kernel_kind_name(int kind);
+int ggnn_profile_begin(int max_launches);
+int ggnn_profile_end(double* total_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GGNN_H */
