@@ -1,0 +1,226 @@
+"""Host-side batching for the bank-to-bank ("btb") task: the producer of the
+propagation path's inputs.
+
+Re-implements, with the same names, arguments and outputs, the numpy data path
+of the reference's ``DenseGGNNChemModel``:
+
+* ``graph_to_adj_mat_bd``      chem_tensorflow_dense.py:65-83
+* ``target_to_adj_mat``        chem_tensorflow_dense.py:93-104
+* ``process_raw_graphs``       chem_tensorflow_dense.py:519-582
+* ``get_bucket_sizes``         chem_tensorflow_dense.py:584-585
+* ``vectorize_node_features``  chem_tensorflow_dense.py:587-613 (btb branch)
+* ``get_mask``                 chem_tensorflow_dense.py:633-660
+* ``get_labels_padded``        chem_tensorflow_dense.py:675-696 (btb branch)
+* ``make_batch``               chem_tensorflow_dense.py:734-773
+* ``make_minibatch_iterator``  chem_tensorflow_dense.py:792-875
+* ``get_word_inputs_padded``, ``get_target_values_edges_formatted``,
+  ``get_target_values_formatted``  chem_tensorflow_dense.py:877-922
+
+Feed dicts are keyed by placeholder NAME (the reference keys them by TF
+placeholder objects whose names are these strings).  Pinned against the
+reference's own helpers by ``tests/golden`` fixtures (tests/test_batching.py).
+The random calls (``np.random.shuffle`` on the global numpy RNG) happen in the
+reference's order so seeded training batches coincide.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+
+import numpy as np
+
+
+def graph_to_adj_mat_bd(graph, max_n_vertices, num_edge_types):
+    """[2E, v, v] float64 adjacency, row = receiving node (see module doc).
+    Vectorised form of chem_tensorflow_dense.py:65-83."""
+    E, v = int(num_edge_types), int(max_n_vertices)
+    amat = np.zeros((2 * E, v, v))
+    if len(graph) == 0:
+        return amat
+    g = np.asarray(graph, dtype=np.int64).reshape(-1, 3)
+    src, lab, dst = g[:, 0], g[:, 1] - 1, g[:, 2]
+    amat[lab, dst, src] = 1            # incoming edge, channel e-1
+    amat[lab + E, src, dst] = 1        # outgoing edge, channel e-1+E
+    amat[E - 1, dst, dst - 1] = 1      # previous-word edge
+    amat[2 * E - 1, dst - 1, dst] = 1  # next-word edge
+    return amat
+
+
+def target_to_adj_mat(target, max_n_vertices, num_edge_types, output_size, tie_fwd_bkwd=True):
+    """[e, v, o] one-hot target heads: node i+1 has head src with label e
+    (chem_tensorflow_dense.py:93-104)."""
+    amat = np.zeros((int(num_edge_types), int(max_n_vertices), int(output_size)))
+    for i, (src, e) in enumerate(target):
+        amat[e - 1, i + 1, src] = 1
+    return amat
+
+
+class BtbBatching:
+    """Mixin with the reference's btb batching API.  Requires the attributes
+    the reference reads from ``self``: ``params`` (batch_size, output_size,
+    task_ids, task_sample_ratios, tie_fwd_bkwd, hidden_size,
+    graph_state_dropout_keep_prob, emb_dropout_keep_prob), ``num_edge_types``,
+    ``output_size_edges``, ``pos_size``, ``bucket_max_nodes``."""
+
+    # ---------------------------------------------------------------- buckets
+    def get_bucket_sizes(self):
+        return np.array(list(range(4, 200, 2)))
+
+    # ------------------------------------------------------------ per graph
+    def get_pos_vector(self, node_feature, deactivate_pos=False):
+        if deactivate_pos:
+            return []
+        vec = [0] * self.pos_size
+        vec[node_feature] = 1
+        return vec
+
+    def get_dep_vector(self, node_edge, deactivate_pos=True):
+        if deactivate_pos:
+            return []
+        vec = [0] * (self.num_edge_types + 1)
+        vec[node_edge[1]] = 1
+        return vec
+
+    def vectorize_node_features(self, node_features, v, graph):
+        """btb: [one-hot(node index) padded to bucket_max_nodes | one-hot(POS)]."""
+        n = len(node_features)
+        width = int(self.bucket_max_nodes) + int(self.pos_size)
+        out = np.zeros((n, width), dtype=np.int64)
+        out[np.arange(n), np.arange(n)] = 1
+        out[np.arange(n), int(self.bucket_max_nodes) + np.asarray(node_features, dtype=np.int64)] = 1
+        return [row for row in out]
+
+    def get_mask(self, n_active_nodes, chosen_bucket_size, is_edge=False):
+        """btb masks: [v*o] with 1 where (i < n and j < n); edge mask [v*e_o]
+        with 1 where i < n (closed form of chem_tensorflow_dense.py:633-660)."""
+        v, n = int(chosen_bucket_size), int(n_active_nodes)
+        if is_edge:
+            m = np.zeros((v, self.output_size_edges))
+            m[:n, :] = 1.0
+            return m.reshape(-1)
+        o = self.params["output_size"]
+        m = np.zeros((v, o))
+        m[:n, :n] = 1.0
+        return m.reshape(-1)
+
+    def get_labels_padded(self, data_dict, chosen_bucket_size, n_active_nodes):
+        return target_to_adj_mat(data_dict["targets"], chosen_bucket_size, self.output_size_edges,
+                                 chosen_bucket_size, self.params.get("tie_fwd_bkwd", True))
+
+    # ------------------------------------------------------------- datasets
+    def process_raw_graphs(self, raw_data, is_training_data, bucket_sizes=None):
+        """Bucket graphs by max node id, densify adjacency per graph.
+        Returns (bucketed, bucket_sizes, bucket_at_step)."""
+        if bucket_sizes is None:
+            bucket_sizes = self.get_bucket_sizes()
+        bucketed = defaultdict(list)
+        for d in raw_data:
+            if len(d["graph"]) == 0:
+                continue
+            max_id = max(max(e[0], e[2]) for e in d["graph"])
+            bidx = int(np.argmax(bucket_sizes > max_id))
+            v = int(bucket_sizes[bidx])
+            n = len(d["node_features"])
+            feats = self.vectorize_node_features(d["node_features"], v, d["graph"])
+            xdim = len(feats[0])
+            heads = [0] + [e[0] for e in d["graph"]]
+            bucketed[bidx].append({
+                "adj_mat": graph_to_adj_mat_bd(d["graph"], v, self.num_edge_types),
+                "init": feats + [np.zeros(xdim, dtype=np.int64) for _ in range(v - n)],
+                "labels": self.get_labels_padded(d, v, n),
+                "mask": self.get_mask(n, v),
+                "mask_edges": self.get_mask(n, v, is_edge=True),
+                "raw_sentence": d.get("raw_sentence"),
+                "id": d.get("id"),
+                "words_pos": d["node_features"],
+                "words_loc": list(range(n)),
+                "words_index": d["words_index"],
+                "words_head": heads,
+                "words_head_pos": [d["node_features"][x] for x in heads],
+                "edges_index": [0] + [e[1] for e in d["graph"]],
+                "target_pos": d["node_features_target"],
+            })
+        if is_training_data:
+            for bidx, bucket in bucketed.items():
+                np.random.shuffle(bucket)
+                for task_id in self.params["task_ids"]:
+                    ratio = self.params.get("task_sample_ratios", {}).get(str(task_id))
+                    if ratio is not None:
+                        for ex in range(int(len(bucket) * ratio), len(bucket)):
+                            bucket[ex]["labels"][task_id] = None
+        bs = self.params["batch_size"]
+        bucket_at_step = [bidx for bidx, data in bucketed.items() for _ in range(1 + (len(data) - 1) // bs)]
+        return bucketed, bucket_sizes, bucket_at_step
+
+    def make_batch(self, elements):
+        keys = ("adj_mat", "init", "node_mask", "node_mask_edges", "sentences_id", "words_pos",
+                "words_loc", "words_index", "words_head", "words_head_pos", "edges_index", "target_pos")
+        batch = {k: [] for k in keys}
+        batch["labels"], batch["task_masks"] = [], []
+        src = {"node_mask": "mask", "node_mask_edges": "mask_edges", "sentences_id": "id"}
+        for d in elements:
+            for k in keys:
+                batch[k].append(d[src.get(k, k)])
+            vals, mask = [], []
+            for tv in d["labels"]:
+                vals.append(0.0 if tv is None else tv)
+                mask.append(0.0 if tv is None else 1.0)
+            batch["labels"].append(vals)
+            batch["task_masks"].append(mask)
+        return batch
+
+    @staticmethod
+    def get_word_inputs_padded(words_pos, b, v):
+        out = np.zeros([b, v])
+        for i, row in enumerate(words_pos):
+            out[i, :len(row)] = row
+        return out
+
+    def get_target_values_edges_formatted(self, labels):
+        lab = np.asarray(labels)                       # [b, e, v', v]
+        b, e, v, _ = lab.shape
+        return lab.sum(axis=3).transpose(0, 2, 1).reshape(b, v * e)
+
+    def get_target_values_formatted(self, labels, no_labels=True):
+        lab = np.asarray(labels)                       # [b, e, v', v]
+        b, e, v, _ = lab.shape
+        o = self.params["output_size"]
+        out = np.zeros((b, v, o))
+        out[:, :, :v] = lab.sum(axis=1)                # sum over e, pad v -> o
+        return out.reshape(b, v * o)
+
+    def make_minibatch_iterator(self, data, is_training):
+        """Yields feed dicts keyed by placeholder name (chem_tensorflow_dense.py:792-875)."""
+        bucketed, bucket_sizes, bucket_at_step = data
+        if is_training:
+            np.random.shuffle(bucket_at_step)
+            for _, bd in bucketed.items():
+                np.random.shuffle(bd)
+        counters = defaultdict(int)
+        bs = self.params["batch_size"]
+        keep = self.params.get("graph_state_dropout_keep_prob", 1.0) if is_training else 1.0
+        emb_keep = self.params.get("emb_dropout_keep_prob", 1.0) if is_training else 1.0
+        for bidx in bucket_at_step:
+            elements = bucketed[bidx][counters[bidx] * bs:(counters[bidx] + 1) * bs]
+            batch = self.make_batch(elements)
+            b, v = len(batch["init"]), int(bucket_sizes[bidx])
+            pad = lambda key: self.get_word_inputs_padded(batch[key], b, v)
+            word_inputs = np.stack((pad("words_loc"), pad("words_pos"), pad("words_index"),
+                                    pad("words_head"), pad("words_head_pos"), pad("edges_index")), axis=2)
+            feed = {
+                "target_values_head": self.get_target_values_formatted(batch["labels"]),
+                "target_values_edges": self.get_target_values_edges_formatted(batch["labels"]),
+                "target_mask": np.transpose(batch["task_masks"], axes=[1, 0]),
+                "num_graphs": b,
+                "num_vertices": v,
+                "adjacency_matrix": batch["adj_mat"],
+                "node_mask": np.array(batch["node_mask"]),
+                "node_mask_edges": np.array(batch["node_mask_edges"]),
+                "graph_state_keep_prob": keep,
+                "edge_weight_dropout_keep_prob": keep,
+                "emb_dropout_keep_prob": emb_keep,
+                "sentences_id": batch["sentences_id"],
+                "word_inputs": word_inputs,
+                "target_pos": pad("target_pos"),
+            }
+            counters[bidx] += 1
+            yield feed

@@ -62,6 +62,7 @@ class PropagationEngine:
         self._batch = None          # (b, v) of the staged adjacency
         self._ws = {}               # (b, v, T, training) -> workspace
         self._trained = None        # (b, v, T, pack, ws) of the last training forward
+        self.generation = 0         # bumped by every forward (autograd staleness check)
 
     # ------------------------------------------------------------------ utils
     def dims(self, b: int, v: int, T: int) -> _lib.GGNNDims:
@@ -141,6 +142,7 @@ class PropagationEngine:
         _lib.check(self._lib.ggnn_forward(ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws),
                                           int(bool(training)), _ptr(h0), _ptr(out), _stream()), "ggnn_forward")
         self._trained = (b, v, T, pack, ws) if training else None
+        self.generation += 1
         return out
 
     def alloc_grads(self, b: int, v: int) -> dict:

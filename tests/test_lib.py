@@ -1,0 +1,63 @@
+"""The C-ABI library builds, loads and exports every symbol include/ggnn.h
+declares; host-only entry points (no GPU) validate dims.  No compute call."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ggnn_amd import build, _lib
+    if build.needs_build():
+        build.build()
+    return _lib.load()
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "ggnn.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(ggnn_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    for s in ("ggnn_forward", "ggnn_backward", "ggnn_set_adjacency", "ggnn_pack_weights",
+              "ggnn_workspace_bytes", "ggnn_last_error"):
+        assert s in syms
+
+
+def test_every_declared_symbol_is_exported(lib):
+    from ggnn_amd import _lib
+    syms = declared_symbols()
+    assert set(syms) == set(_lib.EXPORTED)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_dims_validation_and_sizes(lib):
+    from ggnn_amd import _lib
+    d = _lib.dims(256, 128, 256, 8, 5)
+    _lib.check_dims(d)
+    ws_t = _lib.workspace_bytes(d, True)
+    ws_i = _lib.workspace_bytes(d, False)
+    assert ws_t > ws_i > 0
+    assert _lib.adjacency_bytes(d) >= 2 * 256 * 8 * 128 * 128 * 2
+    assert _lib.weight_pack_bytes(d) >= 2 * 8 * 256 * 256 * 2
+    for bad, code in ((_lib.dims(1, 1, 100, 8, 5), -2), (_lib.dims(1, 129, 256, 8, 5), -2),
+                      (_lib.dims(0, 10, 256, 8, 5), -1), (_lib.dims(1, 10, 256, 8, 0), -1)):
+        rc = lib.ggnn_check_dims(__import__("ctypes").byref(bad))
+        assert rc == code
+        assert lib.ggnn_last_error().decode()
+    with pytest.raises(_lib.GGNNError):
+        _lib.check_dims(_lib.dims(1, 1, 100, 8, 5))
+
+
+def test_null_pointers_are_rejected_without_gpu(lib):
+    import ctypes
+    from ggnn_amd import _lib
+    d = _lib.dims(2, 16, 128, 4, 2)
+    rc = lib.ggnn_forward(ctypes.byref(d), None, None, None, 0, None, None, None)
+    assert rc == -1 and b"NULL" in lib.ggnn_last_error()
