@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CFG = dict(b=256, v=128, h=256, e=4, T=5)
-BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / f16
 HBM_PEAK_GBS = 8000.0
 
 
@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
+                    help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
+                         "parity mode); fp16 / bf16: single 16-bit MFMA operands (reduced precision)")
     args = ap.parse_args()
 
     import torch
@@ -129,7 +132,7 @@ def main():
     h0_d = torch.from_numpy(h0).to(dev)
     w_d = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
     dhT = torch.from_numpy(np.random.default_rng(7 + rank).standard_normal((b, v, h)).astype(np.float32)).to(dev)
-    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev)
+    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision)
     grads = FlatGradients(h, C, True, device=dev)
     gviews = dict(grads.views)
     gviews["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
@@ -195,7 +198,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": {"fp32": "fp32", "fp16": "fp16", "bf16": "bf16"}[args.precision],
+            "precision_note": {"fp32": "fp32-class: every non-exact MFMA operand as an f16 hi/lo limb pair "
+                                       "(3 products), fp32 accumulation; parity <= 1e-3 vs the fp32 reference",
+                               "fp16": "f16 MFMA operands, fp32 accumulation (reduced precision)",
+                               "bf16": "bf16 MFMA operands, fp32 accumulation (reduced precision)"}[args.precision],
             "data": "synthetic (SURVEY §8d generator: Bernoulli(0.1) adjacency on n~U{v/2..v} active nodes, glorot weights)",
             "config": {"workload": "configs[2]: b=256 graphs/GPU, v=128, hidden=256, e=4 (C=8), T=5, fwd+bwd",
                        "global_batch": world * b, "parallelism": "dp%d" % world},

@@ -13,6 +13,9 @@ import threading
 from .build import LIB
 
 GGNN_USE_EDGE_BIAS = 1
+GGNN_FP32_PARITY = 2
+GGNN_FP16 = 4
+PRECISIONS = ("bf16", "fp16", "fp32")
 
 # Every symbol include/ggnn.h declares (checked by tests/test_lib.py).
 EXPORTED = (
@@ -92,8 +95,11 @@ def check(rc: int, what: str) -> None:
         raise GGNNError("%s failed (%d): %s" % (what, rc, msg))
 
 
-def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True) -> GGNNDims:
-    return GGNNDims(int(b), int(v), int(h), int(C), int(T), GGNN_USE_EDGE_BIAS if use_edge_bias else 0)
+def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "bf16") -> GGNNDims:
+    if precision not in PRECISIONS:
+        raise ValueError("precision must be one of %s" % (PRECISIONS,))
+    flags = (GGNN_USE_EDGE_BIAS if use_edge_bias else 0) | {"bf16": 0, "fp16": GGNN_FP16, "fp32": GGNN_FP32_PARITY}[precision]
+    return GGNNDims(int(b), int(v), int(h), int(C), int(T), flags)
 
 
 def check_dims(d: GGNNDims) -> None:

@@ -12,7 +12,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "ggnn_kernels.hip")
+CSRC = os.path.join(HERE, "csrc")
+SRC = os.path.join(CSRC, "ggnn_api.hip")
 LIB = os.path.join(HERE, "libggnn.so")
 HEADER = os.path.join(ROOT, "include", "ggnn.h")
 
@@ -28,7 +29,8 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, HEADER))
+    deps = [HEADER] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h"))]
+    return any(os.path.getmtime(p) > t for p in deps)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

@@ -1,0 +1,562 @@
+// ggnn_api.hip -- host side of libggnn.so: buffer layouts, kernel dispatch and
+// the C ABI declared in include/ggnn.h.  Kernels: k_prep.h, k_prop.h, k_gru.h,
+// k_wgrad.h.  See DESIGN.md for the HBM layout and the roofline per kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/ggnn.h"
+#include "ggnn_common.h"
+#include "k_gru.h"
+#include "k_prep.h"
+#include "k_prop.h"
+#include "k_wgrad.h"
+
+// ---------------------------------------------------------------------------
+// error handling (thread-local last error; no exception crosses the ABI)
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                                      \
+  do {                                                                                                 \
+    hipError_t e_ = (x);                                                                               \
+    if (e_ != hipSuccess) return fail(GGNN_ELAUNCH, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define LAUNCHCHK()                                                                                    \
+  do {                                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                                 \
+    if (e_ != hipSuccess) return fail(GGNN_ELAUNCH, std::string("launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+// ---- optional per-kernel-kind timing with HIP events (bench.py roofline)
+const char* const kKindNames[GGNN_NUM_KERNEL_KINDS] = {
+    "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad"};
+enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD };
+struct ProfState {
+  bool on = false;
+  int cap = 0, used = 0;
+  std::vector<hipEvent_t> ev;  // 2 per record
+  std::vector<int> kind;
+};
+ProfState g_prof;
+struct Prof {
+  int idx = -1;
+  hipStream_t s;
+  Prof(int k, hipStream_t st) : s(st) {
+    if (g_prof.on && g_prof.used < g_prof.cap) {
+      idx = g_prof.used++;
+      g_prof.kind[idx] = k;
+      hipEventRecord(g_prof.ev[2 * idx], s);
+    }
+  }
+  ~Prof() {
+    if (idx >= 0) hipEventRecord(g_prof.ev[2 * idx + 1], s);
+  }
+};
+
+// ---- configuration
+struct Cfg {
+  int b, vin, V, H, C, T, flags;
+  int prec;  // PREC_BF16 / PREC_F16 / PREC_SPLIT
+  bool split;
+  long N;
+  int act;  // bytes per stored activation element
+};
+
+int pad_v(int v) { return v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : -1; }
+
+int make_cfg(const ggnn_dims* d, Cfg* c) {
+  if (!d) return fail(GGNN_EINVAL, "dims is NULL");
+  if (d->b < 1 || d->v < 1 || d->C < 1 || d->T < 1) return fail(GGNN_EINVAL, "dims: b, v, C, T must be >= 1");
+  if (!(d->h == 64 || d->h == 128 || d->h == 256))
+    return fail(GGNN_EUNSUP, "hidden size must be 64, 128 or 256 (got " + std::to_string(d->h) + ")");
+  const int V = pad_v(d->v);
+  if (V < 0) return fail(GGNN_EUNSUP, "v must be <= 128 (got " + std::to_string(d->v) + ")");
+  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16)) return fail(GGNN_EINVAL, "unknown flag bits");
+  if ((d->flags & GGNN_FP32_PARITY) && (d->flags & GGNN_FP16))
+    return fail(GGNN_EINVAL, "GGNN_FP32_PARITY and GGNN_FP16 are exclusive");
+  c->b = d->b; c->vin = d->v; c->V = V; c->H = d->h; c->C = d->C; c->T = d->T; c->flags = d->flags;
+  c->prec = (d->flags & GGNN_FP32_PARITY) ? PREC_SPLIT : (d->flags & GGNN_FP16) ? PREC_F16 : PREC_BF16;
+  c->split = c->prec == PREC_SPLIT;
+  c->act = c->split ? 4 : 2;
+  c->N = (long)d->b * V;
+  if ((double)c->N * c->H * 4 >= 2147483647.0) return fail(GGNN_EUNSUP, "b*v*h too large for 32-bit buffer offsets");
+  return GGNN_OK;
+}
+
+size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// ---- weight pack: bf16 hi part then lo part of every packed operand
+struct PackL {
+  size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, total;
+  long loW, loWg, loWc;  // element offset of the lo part from the hi part
+};
+PackL pack_layout(const Cfg& c) {
+  PackL L;
+  size_t o = 0;
+  const size_t H = c.H;
+  L.loW = (long)c.C * H * H;
+  L.loWg = (long)4 * H * H;
+  L.loWc = (long)2 * H * H;
+  L.Wf = o;   o += al(2 * c.C * H * H * 2);
+  L.WT = o;   o += al(2 * c.C * H * H * 2);
+  L.beta = o; o += al(c.C * H * 4);
+  L.Wg = o;   o += al(2 * 4 * H * H * 2);
+  L.WgT = o;  o += al(2 * 4 * H * H * 2);
+  L.Wc = o;   o += al(2 * 2 * H * H * 2);
+  L.WcT = o;  o += al(2 * 2 * H * H * 2);
+  L.bg = o;   o += al(2 * H * 4);
+  L.bc = o;   o += al(H * 4);
+  L.total = o;
+  return L;
+}
+
+// ---- staged adjacency
+struct AdjL {
+  size_t Ab, AbT, deg, total;
+};
+AdjL adj_layout(const Cfg& c) {
+  AdjL L;
+  size_t o = 0;
+  L.Ab = o;  o += al((size_t)c.b * c.C * c.V * c.V * 2);
+  L.AbT = o; o += al((size_t)c.b * c.C * c.V * c.V * 2);
+  L.deg = o; o += al((size_t)c.b * c.C * c.V * 4);
+  L.total = o;
+  return L;
+}
+
+// ---- per-batch workspace
+struct WsL {
+  size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
+  size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
+  size_t dA, dB, dXT, dzcT, dzgT, dMT;
+  size_t nh4, nha;                 // bytes of one [N][H] fp32 / activation array
+  size_t total;
+};
+WsL ws_layout(const Cfg& c, bool training) {
+  WsL L;
+  memset(&L, 0, sizeof(L));
+  size_t o = 0;
+  const size_t N = c.N, H = c.H, T = c.T, C = c.C;
+  L.nh4 = al(N * H * 4);
+  L.nha = al(N * H * c.act);
+  const size_t nh2 = al(N * H * 2);
+  if (!c.split) {
+    L.hb[0] = o; o += nh2;
+    L.hb[1] = o; o += nh2;
+  }
+  L.Xa = o; o += L.nha;
+  if (!training) {
+    L.hf[0] = o; o += L.nh4;
+    L.hf[1] = o; o += L.nh4;
+  } else {
+    L.hfT = o; o += L.nh4 * (T + 1);
+    L.hT = o;  o += L.nha * T;
+    L.XT = o;  o += L.nha * T;
+    L.rhT = o; o += L.nha * T;
+    L.r = o;   o += L.nh4 * T;
+    L.u = o;   o += L.nh4 * T;
+    L.c = o;   o += L.nh4 * T;
+    L.dA = o;  o += L.nh4;
+    L.dB = o;  o += L.nh4;
+    L.dXT = o; o += L.nha;
+    L.dzcT = o; o += L.nha * T;
+    L.dzgT = o; o += 2 * L.nha * T;
+    L.dMT = o;  o += C * L.nha * T;
+  }
+  L.total = o;
+  return L;
+}
+
+template <typename T> T* P(void* base, size_t off) { return (T*)((char*)base + off); }
+template <typename T> const T* P(const void* base, size_t off) { return (const T*)((const char*)base + off); }
+int grid1d(long n, int bs = 256) {
+  const long g = (n + bs - 1) / bs;
+  return (int)std::min<long>(std::max<long>(g, 1), 8192);
+}
+
+// ---- dispatch helpers
+// rows per GRU workgroup = 32*RT; RT capped per kernel by its VGPR budget
+int gru_rt(const Cfg& c, int maxrt) {
+  const long t = c.N / 32;
+  if (maxrt >= 4 && t % 4 == 0) return 4;
+  if (maxrt >= 2 && t % 2 == 0) return 2;
+  return 1;
+}
+
+template <int V, int H, int PREC>
+void launch_prop_fwd(const Cfg& c, const void* hs, const u16* Ab, const PackL& PL, const void* pk, void* Xa, void* XT,
+                     hipStream_t s) {
+  Prof p(K_PROP_FWD, s);
+  hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab,
+                     P<u16>(pk, PL.Wf), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (ActT<PREC>*)XT, c.C, c.N);
+}
+template <int V, int H, int PREC>
+void launch_prop_bwd(const Cfg& c, const void* dXT, const u16* AbT, const float* deg, const PackL& PL, const void* pk,
+                     const float* dh_in, float* dh_out, void* dMT, float* dbeta, hipStream_t s) {
+  Prof p(K_PROP_BWD, s);
+  hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
+                     P<u16>(pk, PL.WT), PL.loW, dh_in, dh_out, (ActT<PREC>*)dMT, dbeta, c.C, c.N);
+}
+template <int H, int RT, int PREC>
+void launch_gru_fwd(const Cfg& c, const void* Xa, const u16* hb, const float* hf, const PackL& PL, const void* pk,
+                    float* hf_out, u16* hb_out, void* hT, float* r, float* u, float* cc, void* rhT, hipStream_t s) {
+  Prof p(K_GRU_FWD, s);
+  hipLaunchKernelGGL((k_gru_fwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, (const ActT<PREC>*)Xa, hb,
+                     hf, P<u16>(pk, PL.Wg), P<float>(pk, PL.bg), P<u16>(pk, PL.Wc), P<float>(pk, PL.bc), PL.loWg,
+                     PL.loWc, hf_out, hb_out, (ActT<PREC>*)hT, r, u, cc, (ActT<PREC>*)rhT, c.N);
+}
+template <int H, int RT, int PREC>
+void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
+                    const PackL& PL, const void* pk, void* dXT, float* dh_out, void* dzcT, void* dzgT, float* dbc,
+                    float* dbg, hipStream_t s) {
+  Prof p(K_GRU_BWD, s);
+  hipLaunchKernelGGL((k_gru_bwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, delta, hf, r, u, cc,
+                     P<u16>(pk, PL.WcT), P<u16>(pk, PL.WgT), PL.loWc, PL.loWg, (ActT<PREC>*)dXT, dh_out,
+                     (ActT<PREC>*)dzcT, (ActT<PREC>*)dzgT, dbc, dbg, c.N);
+}
+
+#define DISPATCH_V(c, FN, H, PREC, ...)                 \
+  do {                                                  \
+    if ((c).V == 32) FN<32, H, PREC>(__VA_ARGS__);      \
+    else if ((c).V == 64) FN<64, H, PREC>(__VA_ARGS__); \
+    else FN<128, H, PREC>(__VA_ARGS__);                 \
+  } while (0)
+#define DISPATCH_VH(c, FN, PREC, ...)                                  \
+  do {                                                                 \
+    if ((c).H == 64) DISPATCH_V(c, FN, 64, PREC, __VA_ARGS__);         \
+    else if ((c).H == 128) DISPATCH_V(c, FN, 128, PREC, __VA_ARGS__);  \
+    else DISPATCH_V(c, FN, 256, PREC, __VA_ARGS__);                    \
+  } while (0)
+#define DISPATCH_RT(c, FN, H, PREC, ...)                                             \
+  do {                                                                               \
+    constexpr bool sp_ = Prec<PREC>::split;                                          \
+    const int rt_ = gru_rt(c, sp_ ? 2 : kMaxRT<FN##_tag, H>::value);                 \
+    if (!sp_ && rt_ == 4) FN<H, sp_ ? 2 : 4, PREC>(__VA_ARGS__);                     \
+    else if (rt_ == 2) FN<H, 2, PREC>(__VA_ARGS__);                                  \
+    else FN<H, 1, PREC>(__VA_ARGS__);                                                \
+  } while (0)
+#define DISPATCH_HRT(c, FN, PREC, ...)                                 \
+  do {                                                                 \
+    if ((c).H == 64) DISPATCH_RT(c, FN, 64, PREC, __VA_ARGS__);        \
+    else if ((c).H == 128) DISPATCH_RT(c, FN, 128, PREC, __VA_ARGS__); \
+    else DISPATCH_RT(c, FN, 256, PREC, __VA_ARGS__);                   \
+  } while (0)
+
+// RT caps: the fused GRU backward at H = 256 keeps a1/a2 (2 x 16 x RT fp32
+// registers) live through both products and spills at RT = 4.
+struct launch_gru_fwd_tag {};
+struct launch_gru_bwd_tag {};
+template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
+template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
+
+void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,
+                 int batch, hipStream_t s) {
+  const int total = (N / 32) * (K / 16) * 64;
+  Prof p(K_PACK, s);
+  if (f16)
+    hipLaunchKernelGGL(k_pack_B<true>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out, sO, lo);
+  else
+    hipLaunchKernelGGL(k_pack_B<false>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out, sO, lo);
+}
+
+// -------------------------------------------------------------------- forward
+template <int PREC>
+int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool tr, const float* h0, float* hT,
+                 hipStream_t s) {
+  typedef ActT<PREC> Act;
+  constexpr bool SPLIT = Prec<PREC>::split;
+  const WsL L = ws_layout(c, tr);
+  const PackL PL = pack_layout(c);
+  const AdjL AL = adj_layout(c);
+  const long N = c.N, H = c.H;
+  float* hf0 = tr ? P<float>(ws, L.hfT) : P<float>(ws, L.hf[0]);
+  {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H, hf0,
+                       SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N, (int)Prec<PREC>::f16);
+  }
+  if (tr) {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL((k_transpose<float, Act, Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, hf0,
+                       P<Act>(ws, L.hT), N, c.H);
+  }
+  for (int t = 0; t < c.T; ++t) {
+    const float* hf_in = tr ? P<float>(ws, L.hfT + L.nh4 * t) : P<float>(ws, L.hf[t & 1]);
+    float* hf_out = tr ? P<float>(ws, L.hfT + L.nh4 * (t + 1)) : P<float>(ws, L.hf[(t + 1) & 1]);
+    const u16* hb_in = SPLIT ? nullptr : P<u16>(ws, L.hb[t & 1]);
+    u16* hb_out = SPLIT ? nullptr : P<u16>(ws, L.hb[(t + 1) & 1]);
+    const void* hs = SPLIT ? (const void*)hf_in : (const void*)hb_in;
+    void* XT = tr ? P<void>(ws, L.XT + L.nha * t) : nullptr;
+    DISPATCH_VH(c, launch_prop_fwd, PREC, c, hs, P<u16>(adj, AL.Ab), PL, pack, P<void>(ws, L.Xa), XT, s);
+    void* hTo = (tr && t + 1 < c.T) ? P<void>(ws, L.hT + L.nha * (t + 1)) : nullptr;
+    float* ro = tr ? P<float>(ws, L.r + L.nh4 * t) : nullptr;
+    float* uo = tr ? P<float>(ws, L.u + L.nh4 * t) : nullptr;
+    float* co = tr ? P<float>(ws, L.c + L.nh4 * t) : nullptr;
+    void* rhT = tr ? P<void>(ws, L.rhT + L.nha * t) : nullptr;
+    DISPATCH_HRT(c, launch_gru_fwd, PREC, c, P<void>(ws, L.Xa), hb_in, hf_in, PL, pack, hf_out, hb_out, hTo, ro, uo, co,
+                 rhT, s);
+  }
+  const float* hfin = tr ? P<float>(ws, L.hfT + L.nh4 * c.T) : P<float>(ws, L.hf[c.T & 1]);
+  {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, hfin, c.vin, c.V, c.H, hT,
+                       (long)c.b);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+// ------------------------------------------------------------------- backward
+template <int PREC>
+int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, const float* dhT, float* dh0, float* dW,
+                  float* dbeta, float* dWg, float* dbg, float* dWc, float* dbc, hipStream_t s) {
+  const WsL L = ws_layout(c, true);
+  const PackL PL = pack_layout(c);
+  const AdjL AL = adj_layout(c);
+  const long N = c.N, H = c.H;
+  const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
+
+  HIPCHK(hipMemsetAsync(dW, 0, (size_t)c.C * H * H * 4, s));
+  if (use_bias) HIPCHK(hipMemsetAsync(dbeta, 0, (size_t)c.C * H * 4, s));
+  HIPCHK(hipMemsetAsync(dWg, 0, (size_t)4 * H * H * 4, s));
+  HIPCHK(hipMemsetAsync(dbg, 0, (size_t)2 * H * 4, s));
+  HIPCHK(hipMemsetAsync(dWc, 0, (size_t)2 * H * H * 4, s));
+  HIPCHK(hipMemsetAsync(dbc, 0, (size_t)H * 4, s));
+
+  float* dA = P<float>(ws, L.dA);
+  float* dB = P<float>(ws, L.dB);
+  {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0);
+  }
+  for (int t = c.T - 1; t >= 0; --t) {
+    DISPATCH_HRT(c, launch_gru_bwd, PREC, c, dA, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
+                 P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
+                 P<void>(ws, L.dzcT + L.nha * t), P<void>(ws, L.dzgT + 2 * L.nha * t), dbc, dbg, s);
+    DISPATCH_VH(c, launch_prop_bwd, PREC, c, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<float>(adj, AL.deg), PL, pack,
+                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nha * t), use_bias ? dbeta : nullptr, s);
+  }
+  {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
+                       (long)c.b);
+  }
+
+  // weight gradients: out[m][n] += sum_{t,rows} P_t[m][row] Q_t[n][row]
+  if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
+  WgArgs a;
+  memset(&a, 0, sizeof(a));
+  int np = 0, tiles = 0;
+  const long sa = (long)(L.nha / c.act);  // elements of one [H][N] activation array
+  auto add = [&](size_t Poff, long stepP, size_t Qoff, long stepQ, float* out, int ldO, int M, int Nn, int nb = 1,
+                 long sQb = 0, long sOb = 0) {
+    WgProb& p = a.p[np++];
+    p.P = P<void>(ws, Poff);
+    p.Q = P<void>(ws, Qoff);
+    p.out = out;
+    p.ldP = N; p.ldQ = N; p.stepP = stepP; p.stepQ = stepQ; p.sQb = sQb; p.sOb = sOb;
+    p.ldO = ldO; p.M = M; p.N = Nn; p.tiles_n = Nn / 128; p.tiles_b = (M / 128) * p.tiles_n;
+    p.tile_begin = tiles;
+    tiles += nb * p.tiles_b;
+  };
+  // d gates_kernel: rows [0,H) from X, rows [H,2H) from h ; columns dzg (2H)
+  add(L.XT, sa, L.dzgT, 2 * sa, dWg, 2 * H, H, 2 * H);
+  add(L.hT, sa, L.dzgT, 2 * sa, dWg + H * 2 * H, 2 * H, H, 2 * H);
+  // d candidate_kernel: rows [0,H) from X, rows [H,2H) from r*h ; columns dzc (H)
+  add(L.XT, sa, L.dzcT, sa, dWc, H, H, H);
+  add(L.rhT, sa, L.dzcT, sa, dWc + H * H, H, H, H);
+  // d edge_weights[c] = sum_t h_t^T dM_{c,t}: one problem batched over the C channels
+  add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
+  a.nprob = np;
+  a.T = c.T;
+  int KC = 4096;
+  while (KC > 32 && (N % KC) != 0) KC /= 2;
+  while (KC > 256 && (long)tiles * (N / KC) < 256) KC /= 2;
+  if (N % KC) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
+  a.KC = KC;
+  a.nchunks = (int)(N / KC);
+  const int grid = tiles * a.nchunks;
+  {
+    Prof p(K_WGRAD, s);
+    if (Prec<PREC>::split || KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, PREC>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad<64, PREC>), dim3(grid), dim3(256), 0, s, a);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int ggnn_version(void) { return 2; }
+const char* ggnn_last_error(void) { return g_err.c_str(); }
+
+const char* ggnn_kernel_kind_name(int kind) {
+  return (kind >= 0 && kind < GGNN_NUM_KERNEL_KINDS) ? kKindNames[kind] : "";
+}
+
+int ggnn_profile_begin(int max_launches) {
+  if (max_launches < 1) return fail(GGNN_EINVAL, "profile_begin: max_launches < 1");
+  for (hipEvent_t e : g_prof.ev)
+    if (e) hipEventDestroy(e);
+  g_prof.ev.assign(2 * (size_t)max_launches, nullptr);
+  g_prof.kind.assign(max_launches, 0);
+  for (auto& e : g_prof.ev) HIPCHK(hipEventCreate(&e));
+  g_prof.cap = max_launches;
+  g_prof.used = 0;
+  g_prof.on = true;
+  return GGNN_OK;
+}
+
+int ggnn_profile_end(double* total_ms, int* launches) {
+  if (!g_prof.on) return fail(GGNN_EINVAL, "profile_end without profile_begin");
+  g_prof.on = false;
+  for (int k = 0; k < GGNN_NUM_KERNEL_KINDS; ++k) {
+    if (total_ms) total_ms[k] = 0.0;
+    if (launches) launches[k] = 0;
+  }
+  for (int i = 0; i < g_prof.used; ++i) {
+    HIPCHK(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+    if (total_ms) total_ms[g_prof.kind[i]] += ms;
+    if (launches) launches[g_prof.kind[i]] += 1;
+  }
+  const int overflow = g_prof.used >= g_prof.cap;
+  g_prof.used = 0;
+  return overflow ? fail(GGNN_EINVAL, "profile buffer full: raise max_launches") : GGNN_OK;
+}
+
+int ggnn_check_dims(const ggnn_dims* d) {
+  Cfg c;
+  return make_cfg(d, &c);
+}
+
+int ggnn_workspace_bytes(const ggnn_dims* d, int training, size_t* bytes) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!bytes) return fail(GGNN_EINVAL, "bytes is NULL");
+  *bytes = ws_layout(c, training != 0).total;
+  return GGNN_OK;
+}
+
+int ggnn_adjacency_bytes(const ggnn_dims* d, size_t* bytes) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!bytes) return fail(GGNN_EINVAL, "bytes is NULL");
+  *bytes = adj_layout(c).total;
+  return GGNN_OK;
+}
+
+int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!bytes) return fail(GGNN_EINVAL, "bytes is NULL");
+  *bytes = pack_layout(c).total;
+  return GGNN_OK;
+}
+
+int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const float* beta, const float* Wg,
+                      const float* bg, const float* Wc, const float* bc, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!pack || !W || !Wg || !bg || !Wc || !bc) return fail(GGNN_EINVAL, "pack_weights: NULL pointer");
+  if ((c.flags & GGNN_USE_EDGE_BIAS) && !beta)
+    return fail(GGNN_EINVAL, "pack_weights: edge_biases NULL with USE_EDGE_BIAS");
+  hipStream_t s = (hipStream_t)stream;
+  const PackL L = pack_layout(c);
+  const int H = c.H;
+  launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 0, P<u16>(pack, L.Wf), (long)H * H, L.loW, c.C, s);      // MT: Bmat = W_c
+  launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 1, P<u16>(pack, L.WT), (long)H * H, L.loW, c.C, s);      // dh: Bmat = W_c^T
+  launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, s);
+  launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, s);
+  launch_pack(c.prec != PREC_BF16, Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, s);   // Bmat = Wc   [2H][H]
+  launch_pack(c.prec != PREC_BF16, Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, s);  // Bmat = Wc^T [H][2H]
+  {
+    Prof p(K_PACK, s);
+    const float* bsrc = (c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr;
+    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d((long)c.C * H)), dim3(256), 0, s, bsrc, P<float>(pack, L.beta),
+                       (long)c.C * H);
+    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(2 * H)), dim3(256), 0, s, bg, P<float>(pack, L.bg), (long)2 * H);
+    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(H)), dim3(256), 0, s, bc, P<float>(pack, L.bc), (long)H);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!adj || !A) return fail(GGNN_EINVAL, "set_adjacency: NULL pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const AdjL L = adj_layout(c);
+  const dim3 grid((unsigned)(c.b * c.C));
+  Prof p(K_ADJ, s);
+#define PREP_ADJ(VV, F)                                                                                       \
+  hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT), \
+                     P<float>(adj, L.deg))
+  if (c.prec != PREC_BF16) {
+    if (c.V == 32) PREP_ADJ(32, true);
+    else if (c.V == 64) PREP_ADJ(64, true);
+    else PREP_ADJ(128, true);
+  } else {
+    if (c.V == 32) PREP_ADJ(32, false);
+    else if (c.V == 64) PREP_ADJ(64, false);
+    else PREP_ADJ(128, false);
+  }
+#undef PREP_ADJ
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_forward(const ggnn_dims* d, const void* pack, const void* adj, void* ws, int training, const float* h0,
+                 float* hT, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!pack || !adj || !ws || !h0 || !hT) return fail(GGNN_EINVAL, "forward: NULL pointer");
+  hipStream_t s = (hipStream_t)stream;
+  switch (c.prec) {
+    case PREC_SPLIT: return forward_impl<PREC_SPLIT>(c, pack, adj, ws, training != 0, h0, hT, s);
+    case PREC_F16: return forward_impl<PREC_F16>(c, pack, adj, ws, training != 0, h0, hT, s);
+    default: return forward_impl<PREC_BF16>(c, pack, adj, ws, training != 0, h0, hT, s);
+  }
+}
+
+int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* ws, const float* dhT, float* dh0,
+                  float* dW, float* dbeta, float* dWg, float* dbg, float* dWc, float* dbc, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!pack || !adj || !ws || !dhT || !dh0 || !dW || !dWg || !dbg || !dWc || !dbc)
+    return fail(GGNN_EINVAL, "backward: NULL pointer");
+  if ((c.flags & GGNN_USE_EDGE_BIAS) && !dbeta)
+    return fail(GGNN_EINVAL, "backward: d_edge_biases NULL with USE_EDGE_BIAS");
+  hipStream_t s = (hipStream_t)stream;
+  switch (c.prec) {
+    case PREC_SPLIT: return backward_impl<PREC_SPLIT>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+    case PREC_F16: return backward_impl<PREC_F16>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+    default: return backward_impl<PREC_BF16>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,196 @@
+// ggnn_common.h -- device helpers shared by the GGNN kernels (gfx950 / CDNA4).
+//
+// MFMA fragment maps of v_mfma_f32_32x32x16_bf16 (the only matrix instruction
+// used):
+//   A[32x16]: lane l holds A[l&31][8*(l>>5) + j], j = 0..7
+//   B[16x32]: lane l holds B[8*(l>>5) + j][l&31]
+//   C/D     : lane l, reg r holds D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]
+// An accumulator tile is reused as the next product's B operand when the next
+// product contracts over its ROW index: k-step s takes regs 8s..8s+7, and
+// element j of lane-half hh is row 16s + 8(j>>2) + 4hh + (j&3).
+//
+// Precision policy (template parameter PREC):
+//   PREC = 0  "bf16": operands rounded to bf16, fp32 accumulation;
+//             activations between kernels stored as bf16.
+//   PREC = 1  "fp16": the same with f16 operands (3 more mantissa bits, same
+//             MFMA rate; the path's operands are range-bounded, |x| << 65504).
+//   PREC = 2  "fp32-class" (SPLIT): every non-exact operand x is carried as two
+//                  fp16 limbs x_hi = f16(x), x_lo = f16(x - x_hi) (~22-bit
+//                  mantissa); a product is a_hi*b_hi + a_hi*b_lo + a_lo*b_hi
+//                  on v_mfma_f32_32x32x16_f16 (3 MFMAs, 2 when one side is
+//                  exact, e.g. the 0/1 adjacency); activations between kernels
+//                  stored as fp32.  The f16 range (|x| < 65504) covers every
+//                  operand of the path (|h| < 1, |W| < 1, |X|, |M|, |dz| << 1e4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+typedef uint16_t u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// an MFMA A/B operand fragment: 8 x 16-bit (bf16 or f16 limbs)
+typedef uint4 frag;
+
+#define DEV __device__ __forceinline__
+
+enum { PREC_BF16 = 0, PREC_F16 = 1, PREC_SPLIT = 2 };
+template <int PREC> struct Prec {
+  static constexpr bool split = PREC == PREC_SPLIT;  // two f16 limbs per operand
+  static constexpr bool f16 = PREC != PREC_BF16;     // limb format
+};
+// storage type of activations passed between kernels: limbs, or fp32 (split)
+template <int PREC>
+using ActT = typename std::conditional<Prec<PREC>::split, float, u16>::type;
+
+DEV u16 f2bf(float x) { return __builtin_bit_cast(u16, (__bf16)x); }
+DEV float bf2f(u16 x) { return __uint_as_float(((uint32_t)x) << 16); }
+DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// ---- 16-bit operand limbs: bf16 (F16 = false) or f16 (F16 = true)
+template <bool F16> DEV u16 to_limb(float x) {
+  if constexpr (F16) return __builtin_bit_cast(u16, (_Float16)x);
+  else return f2bf(x);
+}
+template <bool F16> DEV float from_limb(u16 x) {
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, x);
+  else return bf2f(x);
+}
+// residual of the limb rounding of x
+template <bool F16> DEV float lo_part(float x) { return x - from_limb<F16>(to_limb<F16>(x)); }
+template <bool F16> DEV uint32_t pk(float a, float b) {
+  return (uint32_t)to_limb<F16>(a) | ((uint32_t)to_limb<F16>(b) << 16);
+}
+template <bool F16> DEV uint32_t pk_lo(float a, float b) { return pk<F16>(lo_part<F16>(a), lo_part<F16>(b)); }
+template <bool F16> DEV frag pk8(const float* x) {
+  return make_uint4(pk<F16>(x[0], x[1]), pk<F16>(x[2], x[3]), pk<F16>(x[4], x[5]), pk<F16>(x[6], x[7]));
+}
+template <bool F16> DEV frag pk8_lo(const float* x) {
+  return make_uint4(pk_lo<F16>(x[0], x[1]), pk_lo<F16>(x[2], x[3]), pk_lo<F16>(x[4], x[5]), pk_lo<F16>(x[6], x[7]));
+}
+template <bool F16> DEV float limb_elem(frag f, int j) {
+  const uint32_t w = (j < 2) ? f.x : (j < 4) ? f.y : (j < 6) ? f.z : f.w;
+  return from_limb<F16>((u16)((j & 1) ? (w >> 16) : (w & 0xffff)));
+}
+
+template <bool F16> DEV f32x16 mfma(frag a, frag b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+DEV f32x16 splat(float x) {
+  f32x16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = x;
+  return r;
+}
+DEV float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
+DEV float tanh_f(float x) { return 1.0f - 2.0f / (__expf(2.0f * x) + 1.0f); }
+DEV constexpr int acc_row0(int r) { return (r & 3) + 8 * (r >> 2); }
+DEV int acc_row(int r, int hh) { return acc_row0(r) + 4 * hh; }
+
+// operand fragment(s) of k-step s taken from an accumulator tile
+template <bool F16> DEV frag acc_hi(const f32x16& a, int s) {
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = a[8 * s + j];
+  return pk8<F16>(x);
+}
+template <bool F16> DEV frag acc_lo(const f32x16& a, int s) {
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = a[8 * s + j];
+  return pk8_lo<F16>(x);
+}
+
+// D += A*B with the precision policy (split: f16 limbs, 3 products)
+template <int PREC>
+DEV void mma(f32x16& acc, frag ah, frag al, frag bh, frag bl) {
+  if constexpr (Prec<PREC>::split) {
+    acc = mfma<true>(al, bh, acc);
+    acc = mfma<true>(ah, bl, acc);
+  }
+  acc = mfma<Prec<PREC>::f16>(ah, bh, acc);
+}
+// D += A*B where A is exact in the limb format (0/1 adjacency)
+template <int PREC>
+DEV void mma_xa(f32x16& acc, frag a, frag bh, frag bl) {
+  if constexpr (Prec<PREC>::split) acc = mfma<true>(a, bl, acc);
+  acc = mfma<Prec<PREC>::f16>(a, bh, acc);
+}
+// D += A*B where B is exact in the limb format
+template <int PREC>
+DEV void mma_xb(f32x16& acc, frag ah, frag al, frag b) {
+  if constexpr (Prec<PREC>::split) acc = mfma<true>(al, b, acc);
+  acc = mfma<Prec<PREC>::f16>(ah, b, acc);
+}
+
+// XOR swizzle of 16-byte chunks inside rows of NCH chunks so that the 32
+// distinct rows of one MFMA operand read land on distinct LDS bank slots.
+template <int NCH>
+struct Swz {
+  static constexpr int M = (NCH % 16 == 0) ? 15 : (NCH % 8 == 0) ? 7 : (NCH % 4 == 0) ? 3 : 0;
+  static DEV int off(int row, int ch) { return row * NCH * 16 + ((ch ^ (row & M)) << 4); }
+  static DEV int eoff(int row, int e) { return off(row, e >> 3) + ((e & 7) << 1); }
+};
+
+DEV uint4 ld16(const void* p) { return *(const uint4*)p; }
+DEV void st16(void* p, uint4 v) { *(uint4*)p = v; }
+DEV frag lds_frag(const char* img, int off) { return ld16(img + off); }
+
+// B-operand fragment of a packed matrix: [strip][kstep][64 lanes][8] limbs
+DEV frag frag_ld(const u16* base, int strip, int ks, int nks, int lane) {
+  return ld16(base + ((size_t)(strip * nks + ks) * 64 + lane) * 8);
+}
+
+// Raw buffer access with an SRD built from wave-uniform values: one 32-bit
+// voffset VGPR per lane, per-element constants in the SGPR soffset.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+DEV rsrc_t mkrsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+DEV float bld(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+DEV void bst(rsrc_t r, float v, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
+}
+
+// ---- block-cooperative staging of a row-major [R][K] activation tile into
+// swizzled LDS image(s): bf16 -> one image; fp32 -> hi and lo images.
+template <int PREC, int R, int K, int NT>
+DEV void stage_rows(char* hi, char* lo, const ActT<PREC>* src, long ld, int tid) {
+  constexpr int KCH = K / 8;
+  typedef Swz<KCH> S;
+  for (int q = tid; q < R * KCH; q += NT) {
+    const int row = q / KCH, ch = q % KCH;
+    if constexpr (Prec<PREC>::split) {
+      const float4 a = *(const float4*)(src + row * ld + ch * 8);
+      const float4 b = *(const float4*)(src + row * ld + ch * 8 + 4);
+      const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      st16(hi + S::off(row, ch), pk8<true>(x));
+      st16(lo + S::off(row, ch), pk8_lo<true>(x));
+    } else {
+      st16(hi + S::off(row, ch), ld16(src + row * ld + ch * 8));
+    }
+  }
+}
+
+// ---- store 4 consecutive rows (acc regs 4q..4q+3) of one column into a
+// transposed [col][row] activation array (rows contiguous)
+template <int PREC>
+DEV void st_col4(ActT<PREC>* dst, float a, float b, float c, float d) {
+  if constexpr (Prec<PREC>::split) *(float4*)dst = make_float4(a, b, c, d);
+  else *(uint2*)dst = make_uint2(pk<Prec<PREC>::f16>(a, b), pk<Prec<PREC>::f16>(c, d));
+}
+
+// ---- write one accumulator element (value v at row, column e) into image(s)
+template <int PREC, int NCH>
+DEV void img_put(char* hi, char* lo, int row, int e, float v) {
+  *(u16*)(hi + Swz<NCH>::eoff(row, e)) = to_limb<Prec<PREC>::f16>(v);
+  if constexpr (Prec<PREC>::split) *(u16*)(lo + Swz<NCH>::eoff(row, e)) = to_limb<true>(lo_part<true>(v));
+}

@@ -1,0 +1,305 @@
+// k_gru.h -- TF1 GRUCell (reset-before-matmul) forward and backward, fused.
+//
+// Reference: tf.compat.v1.nn.rnn_cell.GRUCell built at
+// chem_tensorflow_dense.py:237-241, applied at :333 (external TF op):
+//   [r | u] = sigmoid([x, h] @ Wg + bg)        Wg [2H][2H], rows [x ; h]
+//   c       = tanh([x, r*h] @ Wc + bc)         Wc [2H][H],  rows [x ; r*h]
+//   h'      = u*h + (1-u)*c
+// A workgroup owns 32*RT consecutive node rows; wave w owns hidden columns
+// [32w, 32w+32) of r, u and c, so r*h for ALL columns is shared through LDS
+// before the candidate product.
+#pragma once
+#include "ggnn_common.h"
+
+// ===========================================================================
+// k_gru_fwd
+//   pass A: [X | h] @ Wg            -> r, u      (K = 2H)
+//   r*h -> LDS (over the h image), r*h^T -> HBM (training)
+//   pass B: X @ Wc[0:H] + (r*h) @ Wc[H:2H] -> c  (K = 2H)
+//   h' = u*h + (1-u)*tanh(c + bc)
+// ===========================================================================
+template <int H, int RT, int PREC>
+__global__ void __launch_bounds__(2 * H)
+k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const float* __restrict__ hf,
+          const u16* __restrict__ Wgp, const float* __restrict__ bg, const u16* __restrict__ Wcp,
+          const float* __restrict__ bc, long wlo_g, long wlo_c, float* __restrict__ hf_out, u16* __restrict__ hb_out,
+          ActT<PREC>* __restrict__ hT_out, float* __restrict__ r_out, float* __restrict__ u_out,
+          float* __restrict__ c_out, ActT<PREC>* __restrict__ rhT_out, long N) {
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  constexpr int NS = H / 32, NT = 64 * NS, KS = H / 16, R = 32 * RT, HCH = H / 8, KSG = 2 * KS;
+  typedef Swz<HCH> SH;
+  constexpr int NIMG = SPLIT ? 2 : 1;
+  constexpr int IMG = R * H * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NIMG * IMG];
+  char* x_hi = smem;
+  char* x_lo = smem + (SPLIT ? IMG : 0);
+  char* h_hi = smem + NIMG * IMG;
+  char* h_lo = h_hi + (SPLIT ? IMG : 0);
+
+  const int tid = threadIdx.x, lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int n = ns * 32 + l32;
+  const long row0 = (long)blockIdx.x * R;
+
+  stage_rows<PREC, R, H, NT>(x_hi, x_lo, Xa + row0 * H, H, tid);
+  if constexpr (SPLIT) stage_rows<PREC_SPLIT, R, H, NT>(h_hi, h_lo, hf + row0 * H, H, tid);
+  else stage_rows<PREC, R, H, NT>(h_hi, h_lo, hb16 + row0 * H, H, tid);
+  __syncthreads();
+
+  f32x16 ar[RT], au[RT];
+  {
+    const float br = bg[n], bu = bg[H + n];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) { ar[rt] = splat(br); au[rt] = splat(bu); }
+  }
+  // ---- pass A, x rows of Wg
+#pragma unroll 2
+  for (int ks = 0; ks < KS; ++ks) {
+    const frag wrh = frag_ld(Wgp, ns, ks, KSG, lane), wuh = frag_ld(Wgp, NS + ns, ks, KSG, lane);
+    const frag wrl = SPLIT ? frag_ld(Wgp + wlo_g, ns, ks, KSG, lane) : wrh;
+    const frag wul = SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, ks, KSG, lane) : wuh;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
+      const frag ah = lds_frag(x_hi, off), al = SPLIT ? lds_frag(x_lo, off) : ah;
+      mma<PREC>(ar[rt], ah, al, wrh, wrl);
+      mma<PREC>(au[rt], ah, al, wuh, wul);
+    }
+  }
+  // ---- pass A, h rows of Wg
+#pragma unroll 2
+  for (int ks = 0; ks < KS; ++ks) {
+    const frag wrh = frag_ld(Wgp, ns, KS + ks, KSG, lane), wuh = frag_ld(Wgp, NS + ns, KS + ks, KSG, lane);
+    const frag wrl = SPLIT ? frag_ld(Wgp + wlo_g, ns, KS + ks, KSG, lane) : wrh;
+    const frag wul = SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, KS + ks, KSG, lane) : wuh;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
+      const frag ah = lds_frag(h_hi, off), al = SPLIT ? lds_frag(h_lo, off) : ah;
+      mma<PREC>(ar[rt], ah, al, wrh, wrl);
+      mma<PREC>(au[rt], ah, al, wuh, wul);
+    }
+  }
+  const rsrc_t rh_in = mkrsrc(hf + row0 * H, R * H * 4);
+  const int vo = (4 * hh * H + n) * 4;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ar[rt][r] = sigm(ar[rt][r]);
+      au[rt][r] = sigm(au[rt][r]);
+    }
+  __syncthreads();  // every wave is done reading the h image
+  // ---- r*h -> h image(s) and (training) r*h^T
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float rh[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      rh[r] = ar[rt][r] * bld(rh_in, vo, (rt * 32 + acc_row0(r)) * H * 4);
+      img_put<PREC, HCH>(h_hi, h_lo, rt * 32 + acc_row(r, hh), n, rh[r]);
+    }
+    if (rhT_out) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st_col4<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
+                       rh[4 * q + 2], rh[4 * q + 3]);
+    }
+    if (r_out) {
+      const rsrc_t ro = mkrsrc(r_out + row0 * H, R * H * 4);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bst(ro, ar[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
+    }
+  }
+  __syncthreads();
+  // ---- pass B: candidate
+  f32x16 ac[RT];
+  {
+    const float b0 = bc[n];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) ac[rt] = splat(b0);
+  }
+#pragma unroll 2
+  for (int ks = 0; ks < KS; ++ks) {
+    const frag wxh = frag_ld(Wcp, ns, ks, KSG, lane), wrh = frag_ld(Wcp, ns, KS + ks, KSG, lane);
+    const frag wxl = SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : wxh;
+    const frag wrl = SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : wrh;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
+      const frag xh = lds_frag(x_hi, off), xl = SPLIT ? lds_frag(x_lo, off) : xh;
+      const frag qh = lds_frag(h_hi, off), ql = SPLIT ? lds_frag(h_lo, off) : qh;
+      mma<PREC>(ac[rt], xh, xl, wxh, wxl);
+      mma<PREC>(ac[rt], qh, ql, wrh, wrl);
+    }
+  }
+  // ---- blend + outputs
+  const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
+  if constexpr (!SPLIT) __syncthreads();  // the h image is reused to stage h' (bf16) below
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int so = (rt * 32 + acc_row0(r)) * H * 4;
+      const float cc = tanh_f(ac[rt][r]);
+      const float u = au[rt][r];
+      const float hn = u * bld(rh_in, vo, so) + (1.0f - u) * cc;
+      bst(ho, hn, vo, so);
+      if (u_out) {
+        bst(mkrsrc(u_out + row0 * H, R * H * 4), u, vo, so);
+        bst(mkrsrc(c_out + row0 * H, R * H * 4), cc, vo, so);
+      }
+      ac[rt][r] = hn;
+      if constexpr (!SPLIT) *(u16*)(h_hi + SH::eoff(rt * 32 + acc_row(r, hh), n)) = to_limb<F16>(hn);
+    }
+    if (hT_out) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st_col4<PREC>(hT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, ac[rt][4 * q], ac[rt][4 * q + 1],
+                       ac[rt][4 * q + 2], ac[rt][4 * q + 3]);
+    }
+  }
+  if constexpr (!SPLIT) {
+    __syncthreads();
+    for (int q = tid; q < R * HCH; q += NT) {
+      const int row = q / HCH, ch = q % HCH;
+      st16(hb_out + (row0 + row) * H + ch * 8, ld16(h_hi + SH::off(row, ch)));
+    }
+  }
+}
+
+// ===========================================================================
+// k_gru_bwd: backward of the GRUCell, delta = dL/dh'
+//   dzc = delta (1-u) (1-c^2)                      -> LDS, dzc^T, dbc
+//   [dX1 | d(rh)] = dzc @ Wc^T                     (K = H)
+//   dh  = delta u + d(rh) r
+//   dzg = [d(rh) h r(1-r) | delta (h-c) u(1-u)]    -> LDS, dzg^T, dbg
+//   [dX2 | dh2] = dzg @ Wg^T                       (K = 2H)
+//   out: dX^T = (dX1 + dX2)^T, dh + dh2 (fp32)
+// ===========================================================================
+template <int H, int RT, int PREC>
+__global__ void __launch_bounds__(2 * H)
+k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
+          const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
+          const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
+          float* __restrict__ dh_out, ActT<PREC>* __restrict__ dzcT, ActT<PREC>* __restrict__ dzgT,
+          float* __restrict__ dbc, float* __restrict__ dbg, long N) {
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
+  typedef Swz<ZCH> SZ;
+  constexpr int NIMG = SPLIT ? 2 : 1;
+  constexpr int IMG = R * 2 * H * 2;
+  __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG];
+  char* z_hi = smem;
+  char* z_lo = smem + (SPLIT ? IMG : 0);
+
+  const int tid = threadIdx.x, lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int n = ns * 32 + l32;
+  const long row0 = (long)blockIdx.x * R;
+  const uint32_t tbytes = R * H * 4;
+  const long tb0 = row0 * H;
+  const rsrc_t pd = mkrsrc(delta + tb0, tbytes), ph = mkrsrc(hf + tb0, tbytes), pr = mkrsrc(rin + tb0, tbytes),
+               pu = mkrsrc(uin + tb0, tbytes), pc = mkrsrc(cin + tb0, tbytes);
+  const int vo = (4 * hh * H + n) * 4;
+  const long tcol = (long)n * N + row0 + 4 * hh;
+
+  // ---- phase 1: dzc
+  float csum = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float dz[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ro = rt * 32 + acc_row0(4 * q + i);
+        const int so = ro * H * 4;
+        const float d = bld(pd, vo, so), u = bld(pu, vo, so), c = bld(pc, vo, so);
+        dz[i] = d * (1.0f - u) * (1.0f - c * c);
+        csum += dz[i];
+        img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
+      }
+      st_col4<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
+      __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
+    }
+  }
+  csum += __shfl_xor(csum, 32);
+  if (hh == 0) atomicAdd(dbc + n, csum);
+  __syncthreads();
+
+  // ---- product 1: [dX1 | d(rh)] = dzc @ Wc^T
+  f32x16 a1[RT], a2[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) { a1[rt] = splat(0.f); a2[rt] = splat(0.f); }
+#pragma unroll 2
+  for (int ks = 0; ks < KS; ++ks) {
+    const frag b1h = frag_ld(WcTp, ns, ks, KS, lane), b2h = frag_ld(WcTp, NS + ns, ks, KS, lane);
+    const frag b1l = SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : b1h;
+    const frag b2l = SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : b2h;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
+      const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
+      mma<PREC>(a1[rt], ah, al, b1h, b1l);
+      mma<PREC>(a2[rt], ah, al, b2h, b2l);
+    }
+  }
+  __syncthreads();  // dzc reads done
+
+  // ---- phase 2: dh (into a2), dzg
+  float rsum = 0.f, usum = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float zr[4], zu[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * q + i;
+        const int ro = rt * 32 + acc_row0(r);
+        const int so = ro * H * 4;
+        const float d = bld(pd, vo, so), h = bld(ph, vo, so), rr = bld(pr, vo, so), u = bld(pu, vo, so),
+                    c = bld(pc, vo, so);
+        const float drh = a2[rt][r];
+        a2[rt][r] = d * u + drh * rr;
+        zr[i] = drh * h * rr * (1.0f - rr);
+        zu[i] = d * (h - c) * u * (1.0f - u);
+        rsum += zr[i];
+        usum += zu[i];
+        img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
+        img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, H + n, zu[i]);
+      }
+      st_col4<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
+      st_col4<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  rsum += __shfl_xor(rsum, 32);
+  usum += __shfl_xor(usum, 32);
+  if (hh == 0) { atomicAdd(dbg + n, rsum); atomicAdd(dbg + H + n, usum); }
+  __syncthreads();
+
+  // ---- product 2: [dX2 | dh2] = dzg @ Wg^T
+#pragma unroll 2
+  for (int ks = 0; ks < 2 * KS; ++ks) {
+    const frag b1h = frag_ld(WgTp, ns, ks, 2 * KS, lane), b2h = frag_ld(WgTp, NS + ns, ks, 2 * KS, lane);
+    const frag b1l = SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : b1h;
+    const frag b2l = SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : b2h;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
+      const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
+      mma<PREC>(a1[rt], ah, al, b1h, b1l);
+      mma<PREC>(a2[rt], ah, al, b2h, b2l);
+    }
+  }
+  const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      st_col4<PREC>(dXT + tcol + rt * 32 + 8 * q, a1[rt][4 * q], a1[rt][4 * q + 1], a1[rt][4 * q + 2],
+                     a1[rt][4 * q + 3]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bst(pdo, a2[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
+  }
+}

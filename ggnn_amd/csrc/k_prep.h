@@ -1,0 +1,120 @@
+// k_prep.h -- boundary conversion kernels (HBM-bound, small next to the hot
+// kernels): weight packing, adjacency staging, state padding / transposes.
+#pragma once
+#include "ggnn_common.h"
+
+// Pack B operand Bmat[K][N] (Bmat = S or S^T, S row-major fp32, leading dim
+// ldS) into MFMA fragment order [N/32][K/16][64][8] of 16-bit limbs (bf16, or
+// f16 for the split mode), hi part at `out`, lo part (x - limb(x)) at
+// `out + lo_off`.  blockIdx.y selects a matrix of a batch (strides sS / sO).
+template <bool F16>
+__global__ void k_pack_B(const float* __restrict__ S, int ldS, long sS, int K, int N, int trans,
+                         u16* __restrict__ out, long sO, long lo_off) {
+  const int total = (N / 32) * (K / 16) * 64;
+  const float* Sb = S + sS * blockIdx.y;
+  u16* ob = out + sO * blockIdx.y;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    const int lane = q & 63, t = q >> 6;
+    const int nks = K / 16;
+    const int ks = t % nks, strip = t / nks;
+    const int n = strip * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = trans ? Sb[(long)n * ldS + k0 + j] : Sb[(long)(k0 + j) * ldS + n];
+    *(uint4*)(ob + (size_t)q * 8) = pk8<F16>(x);
+    *(uint4*)(ob + lo_off + (size_t)q * 8) = pk8_lo<F16>(x);
+  }
+}
+
+__global__ void k_copy_f32(const float* __restrict__ s, float* __restrict__ d, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    d[i] = s ? s[i] : 0.0f;
+}
+
+// Adjacency [b][C][vin][vin] fp32 -> per (g,c) tile:
+//   Ab  [V][V] bf16, columns permuted inside every 16-column group (8-byte
+//       chunks 1 and 2 swapped) = the k order of an accumulator-as-B operand
+//       (k_prop_fwd's AGG);
+//   AbT [V][V] bf16 = A^T, natural order (B operand of k_prop_bwd);
+//   deg [V] fp32 = row sums (in-degree per channel, for dL/dbeta).
+template <int V, bool F16>
+__global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, int vin,
+                                                  u16* __restrict__ Ab, u16* __restrict__ AbT,
+                                                  float* __restrict__ deg) {
+  __shared__ u16 t[V][V + 2];
+  const long tile = blockIdx.x;  // g*C + c
+  const float* src = A + tile * (long)vin * vin;
+  for (int q = threadIdx.x; q < V * V; q += 256) {
+    const int i = q / V, j = q % V;
+    t[i][j] = to_limb<F16>((i < vin && j < vin) ? src[i * vin + j] : 0.0f);
+  }
+  __syncthreads();
+  u16* ab = Ab + tile * V * V;
+  u16* at = AbT + tile * V * V;
+  for (int q = threadIdx.x; q < V * V; q += 256) {
+    const int i = q / V, p = q % V;
+    const int grp = p & ~15, w = p & 15;
+    const int j = grp + ((w < 4) ? w : (w < 8) ? w + 4 : (w < 12) ? w - 4 : w);
+    ab[q] = t[i][j];
+    at[q] = t[p][i];
+  }
+  if (threadIdx.x < V) {
+    float s = 0.f;
+    for (int j = 0; j < V; ++j) s += from_limb<F16>(t[threadIdx.x][j]);
+    deg[tile * V + threadIdx.x] = s;
+  }
+}
+
+// h0 [b][vin][H] fp32 -> hf [N][H] fp32 (pad rows zero) and optional hb in
+// the limb format (bf16, or f16 when f16 != 0)
+__global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H, float* __restrict__ hf,
+                            u16* __restrict__ hb, long N, int f16) {
+  const long total = N * H;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const long row = q / H;
+    const int col = q % H;
+    const long g = row / V;
+    const int i = row % V;
+    const float x = (i < vin) ? h0[(g * vin + i) * H + col] : 0.0f;
+    if (hf) hf[q] = x;
+    if (hb) hb[q] = f16 ? to_limb<true>(x) : to_limb<false>(x);
+  }
+}
+
+// hf [N][H] fp32 -> out [b][vin][H]
+__global__ void k_unpad_state(const float* __restrict__ hf, int vin, int V, int H, float* __restrict__ out, long b) {
+  const long total = b * vin * (long)H;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const long r = q / H;
+    const int col = q % H;
+    const long g = r / vin;
+    const int i = r % vin;
+    out[q] = hf[(g * V + i) * H + col];
+  }
+}
+
+// [N][H] fp32 -> [H][N] of element type TO (fp32, or 16-bit limbs: f16 if F16
+// else bf16), 64x64 tiles through LDS
+template <typename TI, typename TO, bool F16>
+__global__ void __launch_bounds__(256) k_transpose(const TI* __restrict__ in, TO* __restrict__ out, long N, int H) {
+  __shared__ float t[64][65];
+  const long r0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
+    const int i = q / 64, j = q % 64;
+    float x = 0.f;
+    if (r0 + i < N) {
+      if constexpr (std::is_same<TI, float>::value) x = in[(r0 + i) * H + c0 + j];
+      else x = from_limb<F16>(in[(r0 + i) * H + c0 + j]);
+    }
+    t[i][j] = x;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
+    const int j = q / 64, i = q % 64;
+    if (r0 + i < N) {
+      if constexpr (std::is_same<TO, float>::value) out[(long)(c0 + j) * N + r0 + i] = t[i][j];
+      else out[(long)(c0 + j) * N + r0 + i] = to_limb<F16>(t[i][j]);
+    }
+  }
+}

@@ -1,0 +1,292 @@
+// k_prop.h -- message transform + adjacency aggregation, forward and backward.
+//
+// Reference: compute_timestep_fast, chem_tensorflow_dense.py:391-437
+//   X[g,i,:] = sum_c sum_j A[g,c,i,j] * (h[g,j,:] @ W[c] + beta[c])
+// One workgroup owns one graph (the only coupling between graphs is through
+// the shared weights), wave w owns the 32 hidden columns [32w, 32w+32).
+#pragma once
+#include "ggnn_common.h"
+
+// ===========================================================================
+// k_prop_fwd: per channel c
+//   MT : M_c = h W_c + beta_c                 (K = H; h from LDS, W_c from the
+//                                              packed fragments in L2)
+//   AGG: X  += A_c M_c                        (K = V; M_c stays in registers
+//                                              as the B operand, A_c from LDS)
+// LDS: h image(s) [V][H] + one A_c tile [V][V] (register-staged prefetch of
+// A_{c+1} during MT(c)).
+// Outputs: X [N][H] row-major (GRU operand) and X^T [H][N] (weight-gradient
+// operand, training only).
+// ===========================================================================
+template <int V, int H, int PREC>
+__global__ void __launch_bounds__(2 * H)
+k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, const u16* __restrict__ Wp, long wlo,
+           const float* __restrict__ beta, ActT<PREC>* __restrict__ Xo, ActT<PREC>* __restrict__ XT, int C, long N) {
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  using Act = ActT<PREC>;
+  constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KS = H / 16;
+  constexpr int HCH = H / 8, ACH = V / 8;
+  typedef Swz<HCH> SH;
+  typedef Swz<ACH> SA;
+  constexpr int NIMG = SPLIT ? 2 : 1;
+  constexpr int IMG = V * H * 2;
+  constexpr int A_BYTES = V * V * 2;
+  constexpr int APT = (V * ACH + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + A_BYTES];
+  char* h_hi = smem;
+  char* h_lo = smem + (SPLIT ? IMG : 0);
+  char* abuf = smem + NIMG * IMG;
+
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, ns = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int n = ns * 32 + l32;
+  const long rowg = (long)g * V;
+
+  stage_rows<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
+  const u16* ag = Ab + (long)g * C * V * V;
+  uint4 areg[APT];
+#pragma unroll
+  for (int p = 0; p < APT; ++p) {
+    const int q = tid + p * NT;
+    if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), ld16(ag + q * 8));
+  }
+  __syncthreads();
+
+  f32x16 accx[VT];
+#pragma unroll
+  for (int it = 0; it < VT; ++it) accx[it] = splat(0.f);
+
+  for (int c = 0; c < C; ++c) {
+    const bool pre = (c + 1 < C);
+    if (pre) {
+      const u16* an = ag + (long)(c + 1) * V * V;
+#pragma unroll
+      for (int p = 0; p < APT; ++p) {
+        const int q = tid + p * NT;
+        if (q < V * ACH) areg[p] = ld16(an + q * 8);
+      }
+    }
+    // ---- MT: M_c[j][n] = sum_k h[j][k] W_c[k][n] + beta_c[n]
+    const float bb = beta[c * H + n];
+    f32x16 accm[VT];
+#pragma unroll
+    for (int rt = 0; rt < VT; ++rt) accm[rt] = splat(bb);
+    const u16* wp = Wp + (size_t)c * H * H;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const frag bh = frag_ld(wp, ns, ks, KS, lane);
+      const frag bl = SPLIT ? frag_ld(wp + wlo, ns, ks, KS, lane) : bh;
+#pragma unroll
+      for (int rt = 0; rt < VT; ++rt) {
+        const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
+        const frag ah = lds_frag(h_hi, off);
+        const frag al = SPLIT ? lds_frag(h_lo, off) : ah;
+        mma<PREC>(accm[rt], ah, al, bh, bl);
+      }
+    }
+    __syncthreads();  // S1: A_c visible
+    // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
+#pragma unroll
+    for (int rt = 0; rt < VT; ++rt) {
+      const frag mh0 = acc_hi<F16>(accm[rt], 0), mh1 = acc_hi<F16>(accm[rt], 1);
+      const frag ml0 = SPLIT ? acc_lo<F16>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<F16>(accm[rt], 1) : mh1;
+#pragma unroll
+      for (int it = 0; it < VT; ++it) {
+        const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
+        const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
+        mma_xa<PREC>(accx[it], a0, mh0, ml0);
+        mma_xa<PREC>(accx[it], a1, mh1, ml1);
+      }
+    }
+    __syncthreads();  // S2: A_c reads done
+    if (pre) {
+#pragma unroll
+      for (int p = 0; p < APT; ++p) {
+        const int q = tid + p * NT;
+        if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), areg[p]);
+      }
+    }
+  }
+
+  // ---- X^T (transposed, weight-gradient operand)
+  if (XT) {
+#pragma unroll
+    for (int it = 0; it < VT; ++it)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st_col4<PREC>(XT + (long)n * N + rowg + it * 32 + 8 * q + 4 * hh, accx[it][4 * q], accx[it][4 * q + 1],
+                       accx[it][4 * q + 2], accx[it][4 * q + 3]);
+  }
+  // ---- X row-major through LDS (the h images are free after the last S2)
+  if constexpr (SPLIT) {
+    float* xs = (float*)smem;  // [V][H] fp32 = NIMG*IMG bytes
+#pragma unroll
+    for (int it = 0; it < VT; ++it)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xs[(it * 32 + acc_row(r, hh)) * H + n] = accx[it][r];
+    __syncthreads();
+    for (int q = tid; q < V * H / 4; q += NT) *(float4*)(Xo + rowg * H + q * 4) = ((const float4*)xs)[q];
+  } else {
+#pragma unroll
+    for (int it = 0; it < VT; ++it)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) *(u16*)(h_hi + SH::eoff(it * 32 + acc_row(r, hh), n)) = to_limb<F16>(accx[it][r]);
+    __syncthreads();
+    for (int q = tid; q < V * HCH; q += NT) {
+      const int row = q / HCH, ch = q % HCH;
+      st16(Xo + (rowg + row) * H + ch * 8, ld16(h_hi + SH::off(row, ch)));
+    }
+  }
+}
+
+// ===========================================================================
+// k_prop_bwd: backward of message + aggregation, per channel c
+//   dM_c^T[n][j] = sum_i dX^T[n][i] A_c[i][j]    (K = V; dX^T fragments stay in
+//                                                registers for all channels)
+//   dM_c -> LDS [j][n] image(s); dM_c^T -> HBM (weight-gradient operand)
+//   dh[j][k]   += sum_n dM_c[j][n] W_c[k][n]     (K = H)
+//   dbeta_c[n] += sum_i deg_c[i] dX[i][n]        (= sum_j dM_c[j][n])
+// ===========================================================================
+template <int V, int H, int PREC>
+__global__ void __launch_bounds__(2 * H)
+k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const float* __restrict__ deg,
+           const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
+           ActT<PREC>* __restrict__ dMT, float* __restrict__ dbeta, int C, long N) {
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  using Act = ActT<PREC>;
+  constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
+  constexpr int HCH = H / 8, ACH = V / 8;
+  typedef Swz<HCH> SH;
+  typedef Swz<ACH> SA;
+  constexpr int NIMG = SPLIT ? 2 : 1;
+  constexpr int IMG = V * H * 2, A_BYTES = V * V * 2;
+  constexpr int APT = (V * ACH + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) char smem[A_BYTES + NIMG * IMG];
+  char* abuf = smem;
+  char* m_hi = smem + A_BYTES;
+  char* m_lo = m_hi + (SPLIT ? IMG : 0);
+
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int n = ns * 32 + l32;
+  const long rowg = (long)g * V;
+
+  // dX^T fragments of this wave's 32 columns (A operand of the dM^T product)
+  frag dxh[KV], dxl[KV];
+#pragma unroll
+  for (int s = 0; s < KV; ++s) {
+    const Act* p = dXT + (long)n * N + rowg + 16 * s + 8 * hh;
+    if constexpr (SPLIT) {
+      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      dxh[s] = pk8<true>(x);
+      dxl[s] = pk8_lo<true>(x);
+    } else {
+      dxh[s] = ld16(p);
+      dxl[s] = dxh[s];
+    }
+  }
+
+  const u16* ag = AbT + (long)g * C * V * V;
+  uint4 areg[APT];
+#pragma unroll
+  for (int p = 0; p < APT; ++p) {
+    const int q = tid + p * NT;
+    if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), ld16(ag + q * 8));
+  }
+  const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
+  const int vo = (4 * hh * H + n) * 4;
+  f32x16 adh[VT];
+#pragma unroll
+  for (int jt = 0; jt < VT; ++jt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) adh[jt][r] = bld(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
+  __syncthreads();
+
+  // dM^T store target: element (jt, r) of this lane sits at
+  //   dMT + (c*H + ns*32 + 4hh + acc_row0(r)) * N + rowg + jt*32 + l32
+  for (int c = 0; c < C; ++c) {
+    const bool pre = (c + 1 < C);
+    if (pre) {
+      const u16* an = ag + (long)(c + 1) * V * V;
+#pragma unroll
+      for (int p = 0; p < APT; ++p) {
+        const int q = tid + p * NT;
+        if (q < V * ACH) areg[p] = ld16(an + q * 8);
+      }
+    }
+    if (dbeta) {
+      const float* dg = deg + ((long)g * C + c) * V;
+      float s = 0.f;
+#pragma unroll
+      for (int ss = 0; ss < KV; ++ss) {
+        const float4 d0 = *(const float4*)(dg + 16 * ss + 8 * hh);
+        const float4 d1 = *(const float4*)(dg + 16 * ss + 8 * hh + 4);
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = limb_elem<F16>(dxh[ss], j) + (SPLIT ? limb_elem<F16>(dxl[ss], j) : 0.f);
+        s += d0.x * x[0] + d0.y * x[1] + d0.z * x[2] + d0.w * x[3] + d1.x * x[4] + d1.y * x[5] + d1.z * x[6] +
+             d1.w * x[7];
+      }
+      s += __shfl_xor(s, 32);
+      if (hh == 0) atomicAdd(dbeta + c * H + n, s);
+    }
+    // ---- phase a: dM_c^T tile (rows n of this wave), one 32-column j tile at a time
+#pragma unroll
+    for (int jt = 0; jt < VT; ++jt) {
+      f32x16 am = splat(0.f);
+#pragma unroll
+      for (int s = 0; s < KV; ++s) {
+        const frag b = lds_frag(abuf, SA::off(jt * 32 + l32, 2 * s + hh));
+        mma_xb<PREC>(am, dxh[s], dxl[s], b);
+      }
+      const int j = jt * 32 + l32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = ns * 32 + 8 * q + 4 * hh;
+        *(uint2*)(m_hi + SH::eoff(j, n0)) =
+            make_uint2(pk<F16>(am[4 * q], am[4 * q + 1]), pk<F16>(am[4 * q + 2], am[4 * q + 3]));
+        if constexpr (SPLIT)
+          *(uint2*)(m_lo + SH::eoff(j, n0)) =
+              make_uint2(pk_lo<true>(am[4 * q], am[4 * q + 1]), pk_lo<true>(am[4 * q + 2], am[4 * q + 3]));
+      }
+      if (dMT) {
+        const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
+        const int vm = (int)((((long)ns * 32 + 4 * hh) * N + rowg + j) * sizeof(Act));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int so = (int)(acc_row0(r) * N * sizeof(Act));
+          if constexpr (SPLIT) bst(rdm, am[r], vm, so);
+          else __builtin_amdgcn_raw_buffer_store_b16(to_limb<F16>(am[r]), rdm, vm, so, 0);
+        }
+      }
+    }
+    __syncthreads();  // S1: dM images complete, A_c reads done
+    if (pre) {
+#pragma unroll
+      for (int p = 0; p < APT; ++p) {
+        const int q = tid + p * NT;
+        if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), areg[p]);
+      }
+    }
+    // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
+    const u16* wt = WTp + (size_t)c * H * H;
+#pragma unroll 2
+    for (int ks = 0; ks < KS; ++ks) {
+      const frag bh = frag_ld(wt, ns, ks, KS, lane);
+      const frag bl = SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : bh;
+#pragma unroll
+      for (int jt = 0; jt < VT; ++jt) {
+        const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
+        const frag ah = lds_frag(m_hi, off);
+        const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
+        mma<PREC>(adh[jt], ah, al, bh, bl);
+      }
+    }
+    __syncthreads();  // S2: dM image reads done, A_{c+1} staged
+  }
+  const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
+#pragma unroll
+  for (int jt = 0; jt < VT; ++jt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bst(rdo, adh[jt][r], vo, (jt * 32 + acc_row0(r)) * H * 4);
+}

@@ -1,0 +1,145 @@
+// k_wgrad.h -- weight gradients as one grouped split-K "NT" GEMM launch:
+//   out[m][n] += sum_{t < T} sum_{k in chunk} P_t[m][k] * Q_t[n][k]
+// P_t / Q_t are the transposed activations saved per timestep ([M][K] and
+// [N][K], K = the b*V node rows, contiguous).  Problems (reference autodiff,
+// chem_tensorflow.py:496):
+//   d gates_kernel     = [X | h]^T  dzg        d candidate_kernel = [X | r*h]^T dzc
+//   d edge_weights[c]  = h^T dM_c
+// Each workgroup sums its K chunk over all T steps, then issues one fp32
+// atomicAdd per output element (chip-wide atomic bytes: tiles * chunks * 64 KiB).
+#pragma once
+#include "ggnn_common.h"
+
+struct WgProb {
+  const void* P;
+  const void* Q;
+  float* out;
+  long ldP, ldQ, stepP, stepQ;  // elements
+  long sQb, sOb;                // batch strides of Q and out (batched problem, e.g. one per channel)
+  int ldO, M, N, tiles_n, tiles_b, tile_begin;
+};
+#define WG_MAXP 8
+struct WgArgs {
+  WgProb p[WG_MAXP];
+  int nprob, nchunks, KC, T;
+};
+
+template <int BK, int PREC>
+__global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  using Act = ActT<PREC>;
+  constexpr int CH = BK / 8;                 // 16-B chunks per LDS tile row
+  constexpr int TB = 128 * BK * 2;           // bytes of one bf16 operand image
+  constexpr int NIMG = SPLIT ? 2 : 1;
+  constexpr int BUF = 2 * NIMG * TB;         // P and Q images of one stage
+  constexpr int PT = 128 * CH / 256;         // 8-element chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tile = blockIdx.x / args.nchunks, chunk = blockIdx.x % args.nchunks;
+  int pi = 0;
+  while (pi + 1 < args.nprob && args.p[pi + 1].tile_begin <= tile) ++pi;
+  const WgProb pr = args.p[pi];
+  const int lt0 = tile - pr.tile_begin;
+  const int bi = lt0 / pr.tiles_b, lt = lt0 % pr.tiles_b;
+  const int m0 = (lt / pr.tiles_n) * 128, n0 = (lt % pr.tiles_n) * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int wm = wv >> 1, wn = wv & 1;
+  constexpr int RPB = 256 / (BK * 2);        // tile rows per 256-B LDS bank row
+  auto soff = [&](int row, int ch) { return row * BK * 2 + ((ch ^ ((row / RPB) & (CH - 1))) << 4); };
+
+  const int kits = args.KC / BK, nit = kits * args.T;
+  const long kbase = (long)chunk * args.KC;
+  const Act* Pb = (const Act*)pr.P;
+  const Act* Qb = (const Act*)pr.Q + (long)bi * pr.sQb;
+  float* const outp = pr.out + (long)bi * pr.sOb;
+  // staging registers: one 8-element chunk = 16 B (bf16) or 32 B (fp32)
+  typedef typename std::conditional<SPLIT, float4, uint4>::type V4;
+  constexpr int PER = SPLIT ? 2 : 1;
+  V4 rp[PT][PER], rq[PT][PER];
+  auto gload = [&](int it) {
+    const int t = it / kits;
+    const long k0 = kbase + (long)(it % kits) * BK;
+    const Act* P = Pb + (long)t * pr.stepP;
+    const Act* Q = Qb + (long)t * pr.stepQ;
+#pragma unroll
+    for (int p = 0; p < PT; ++p) {
+      const int q = tid + p * 256, row = q / CH, ch = q % CH;
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        rp[p][e] = *(const V4*)(P + (long)(m0 + row) * pr.ldP + k0 + ch * 8 + 4 * e);
+        rq[p][e] = *(const V4*)(Q + (long)(n0 + row) * pr.ldQ + k0 + ch * 8 + 4 * e);
+      }
+    }
+  };
+  auto put = [&](char* hi, char* lo, int off, const V4* v) {
+    if constexpr (SPLIT) {
+      const float x[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+      st16(hi + off, pk8<true>(x));
+      st16(lo + off, pk8_lo<true>(x));
+    } else {
+      st16(hi + off, v[0]);
+    }
+  };
+  auto sstore = [&](int buf) {
+    char* b = smem + buf * BUF;
+    char* ph = b;
+    char* pl = b + (SPLIT ? TB : 0);
+    char* qh = b + NIMG * TB;
+    char* ql = qh + (SPLIT ? TB : 0);
+#pragma unroll
+    for (int p = 0; p < PT; ++p) {
+      const int q = tid + p * 256, row = q / CH, ch = q % CH;
+      put(ph, pl, soff(row, ch), rp[p]);
+      put(qh, ql, soff(row, ch), rq[p]);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = splat(0.f);
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const bool pre = it + 1 < nit;
+    if (pre) gload(it + 1);
+    const char* b = smem + (it & 1) * BUF;
+    const char* ph = b;
+    const char* pl = b + (SPLIT ? TB : 0);
+    const char* qh = b + NIMG * TB;
+    const char* ql = qh + (SPLIT ? TB : 0);
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      frag ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int off = soff(wm * 64 + i * 32 + l32, 2 * s + hh);
+        ah[i] = lds_frag(ph, off);
+        al[i] = SPLIT ? lds_frag(pl, off) : ah[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int off = soff(wn * 64 + j * 32 + l32, 2 * s + hh);
+        bh[j] = lds_frag(qh, off);
+        bl[j] = SPLIT ? lds_frag(ql, off) : bh[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mma<PREC>(acc[i][j], ah[i], al[i], bh[j], bl[j]);
+    }
+    if (pre) sstore((it + 1) & 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + acc_row(r, hh);
+        const int nn = n0 + wn * 64 + j * 32 + l32;
+        atomicAdd(outp + (long)m * pr.ldO + nn, acc[i][j][r]);
+      }
+}

@@ -52,10 +52,16 @@ class PropagationEngine:
     """Runs ``compute_final_node_representations`` (chem_tensorflow_dense.py:312-340)
     and its backward for batches of shape [b, C, v, v] / [b, v, h]."""
 
-    def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None):
+    def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None,
+                 precision: str = "bf16"):
+        """precision: "bf16" (bf16 MFMA operands, fp32 accumulation) or "fp32"
+        (GGNN_FP32_PARITY: split-bf16 operands, matches fp32 to <= 1e-3)."""
         self.h = int(hidden)
         self.C = int(channels)
         self.use_edge_bias = bool(use_edge_bias)
+        if precision not in _lib.PRECISIONS:
+            raise ValueError("precision must be one of %s" % (_lib.PRECISIONS,))
+        self.precision = precision
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._lib = _lib.load()
         self._adj = None            # staged adjacency buffer
@@ -66,7 +72,7 @@ class PropagationEngine:
 
     # ------------------------------------------------------------------ utils
     def dims(self, b: int, v: int, T: int) -> _lib.GGNNDims:
-        d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias)
+        d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision)
         _lib.check_dims(d)
         return d
 

@@ -46,8 +46,8 @@ class _Propagate(torch.autograd.Function):
                    "gates_kernel": Wg.contiguous(), "gates_bias": bg.contiguous(),
                    "candidate_kernel": Wc.contiguous(), "candidate_bias": bc.contiguous()}
         pack = engine.pack_weights(weights)
-        training = torch.is_grad_enabled() and any(
-            t is not None and t.requires_grad for t in (h0, W, beta, Wg, bg, Wc, bc))
+        # (autograd runs Function.forward with grad mode off: ask the ctx)
+        training = any(ctx.needs_input_grad[:7])
         out = engine.forward(h0.contiguous(), pack, T, training=training)
         ctx.engine = engine
         ctx.generation = engine.generation
@@ -74,7 +74,7 @@ class DenseGGNNChemModel(BtbBatching):
     """Hot-path subset of the reference's DenseGGNNChemModel (btb task)."""
 
     def __init__(self, args=None, params=None, num_edge_types=None, output_size_edges=12, pos_size=46,
-                 bucket_max_nodes=120, device=None, seed=None):
+                 bucket_max_nodes=120, device=None, seed=None, precision="bf16"):
         self.args = dict(args or {"--pr": "btb"})
         self.params = self.default_params()
         if params:
@@ -86,6 +86,7 @@ class DenseGGNNChemModel(BtbBatching):
         self.output_size_edges = int(output_size_edges)
         self.pos_size = int(pos_size)
         self.bucket_max_nodes = int(bucket_max_nodes)
+        self.precision = precision
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.placeholders = {}
         self.weights = {}
@@ -158,7 +159,8 @@ class DenseGGNNChemModel(BtbBatching):
         key = (self.params["hidden_size"], self.num_channels, bool(self.params["use_edge_bias"]), site)
         eng = self._engines.get(key)
         if eng is None:
-            eng = PropagationEngine(key[0], key[1], key[2], device=self.device)  # one per call site
+            eng = PropagationEngine(key[0], key[1], key[2], device=self.device,
+                                    precision=self.precision)  # one per call site
             self._engines[key] = eng
         return eng
 

@@ -60,6 +60,15 @@ enum {
 
 /* flags */
 #define GGNN_USE_EDGE_BIAS 1 /* params['use_edge_bias'], chem_tensorflow_dense.py:158 */
+/* Precision policy (fp32 accumulation in every mode).
+ *   default (0)       bf16 MFMA operands, bf16 activations between kernels
+ *   GGNN_FP16         f16 MFMA operands (3 more mantissa bits, same rate)
+ *   GGNN_FP32_PARITY  every non-exact operand carried as an f16 hi/lo limb
+ *                     pair (3 MFMAs per product, ~22-bit operand mantissa),
+ *                     fp32 activations: matches the reference's fp32
+ *                     arithmetic to <= 1e-3 (tests/test_gpu_parity.py) */
+#define GGNN_FP32_PARITY 2
+#define GGNN_FP16 4
 
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
@@ -67,7 +76,7 @@ typedef struct ggnn_dims {
   int32_t h;     /* hidden size              (params['hidden_size'])        */
   int32_t C;     /* adjacency channels = 2 * num_edge_types                 */
   int32_t T;     /* timesteps (params['num_timesteps'] or fixed_ts)         */
-  int32_t flags; /* GGNN_USE_EDGE_BIAS                                      */
+  int32_t flags; /* GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY or GGNN_FP16      */
 } ggnn_dims;
 
 int ggnn_version(void);
