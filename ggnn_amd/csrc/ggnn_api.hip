@@ -139,7 +139,7 @@ struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
   size_t dA, dB, dXT, dzcT, dzgT, dMT;
-  size_t nh4, nha;                 // bytes of one [N][H] fp32 / activation array
+  size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
 WsL ws_layout(const Cfg& c, bool training) {
@@ -150,6 +150,7 @@ WsL ws_layout(const Cfg& c, bool training) {
   L.nh4 = al(N * H * 4);
   L.nha = al(N * H * c.act);
   const size_t nh2 = al(N * H * 2);
+  L.nhw = nh2;
   if (!c.split) {
     L.hb[0] = o; o += nh2;
     L.hb[1] = o; o += nh2;
@@ -160,18 +161,18 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.hf[1] = o; o += L.nh4;
   } else {
     L.hfT = o; o += L.nh4 * (T + 1);
-    L.hT = o;  o += L.nha * T;
-    L.XT = o;  o += L.nha * T;
-    L.rhT = o; o += L.nha * T;
+    L.hT = o;  o += L.nhw * T;
+    L.XT = o;  o += L.nhw * T;
+    L.rhT = o; o += L.nhw * T;
     L.r = o;   o += L.nh4 * T;
     L.u = o;   o += L.nh4 * T;
     L.c = o;   o += L.nh4 * T;
     L.dA = o;  o += L.nh4;
     L.dB = o;  o += L.nh4;
     L.dXT = o; o += L.nha;
-    L.dzcT = o; o += L.nha * T;
-    L.dzgT = o; o += 2 * L.nha * T;
-    L.dMT = o;  o += C * L.nha * T;
+    L.dzcT = o; o += L.nhw * T;
+    L.dzgT = o; o += 2 * L.nhw * T;
+    L.dMT = o;  o += C * L.nhw * T;
   }
   L.total = o;
   return L;
@@ -198,14 +199,14 @@ void launch_prop_fwd(const Cfg& c, const void* hs, const u16* Ab, const PackL& P
                      hipStream_t s) {
   Prof p(K_PROP_FWD, s);
   hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab,
-                     P<u16>(pk, PL.Wf), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (ActT<PREC>*)XT, c.C, c.N);
+                     P<u16>(pk, PL.Wf), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, const void* dXT, const u16* AbT, const float* deg, const PackL& PL, const void* pk,
                      const float* dh_in, float* dh_out, void* dMT, float* dbeta, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
-                     P<u16>(pk, PL.WT), PL.loW, dh_in, dh_out, (ActT<PREC>*)dMT, dbeta, c.C, c.N);
+                     P<u16>(pk, PL.WT), PL.loW, dh_in, dh_out, (u16*)dMT, dbeta, c.C, c.N);
 }
 template <int H, int RT, int PREC>
 void launch_gru_fwd(const Cfg& c, const void* Xa, const u16* hb, const float* hf, const PackL& PL, const void* pk,
@@ -213,7 +214,7 @@ void launch_gru_fwd(const Cfg& c, const void* Xa, const u16* hb, const float* hf
   Prof p(K_GRU_FWD, s);
   hipLaunchKernelGGL((k_gru_fwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, (const ActT<PREC>*)Xa, hb,
                      hf, P<u16>(pk, PL.Wg), P<float>(pk, PL.bg), P<u16>(pk, PL.Wc), P<float>(pk, PL.bc), PL.loWg,
-                     PL.loWc, hf_out, hb_out, (ActT<PREC>*)hT, r, u, cc, (ActT<PREC>*)rhT, c.N);
+                     PL.loWc, hf_out, hb_out, (u16*)hT, r, u, cc, (u16*)rhT, c.N);
 }
 template <int H, int RT, int PREC>
 void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
@@ -222,7 +223,7 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
   Prof p(K_GRU_BWD, s);
   hipLaunchKernelGGL((k_gru_bwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, delta, hf, r, u, cc,
                      P<u16>(pk, PL.WcT), P<u16>(pk, PL.WgT), PL.loWc, PL.loWg, (ActT<PREC>*)dXT, dh_out,
-                     (ActT<PREC>*)dzcT, (ActT<PREC>*)dzgT, dbc, dbg, c.N);
+                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N);
 }
 
 #define DISPATCH_V(c, FN, H, PREC, ...)                 \
@@ -287,8 +288,8 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   }
   if (tr) {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL((k_transpose<float, Act, Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, hf0,
-                       P<Act>(ws, L.hT), N, c.H);
+    hipLaunchKernelGGL((k_transpose<float, u16, Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, hf0,
+                       P<u16>(ws, L.hT), N, c.H);
   }
   for (int t = 0; t < c.T; ++t) {
     const float* hf_in = tr ? P<float>(ws, L.hfT + L.nh4 * t) : P<float>(ws, L.hf[t & 1]);
@@ -296,13 +297,13 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     const u16* hb_in = SPLIT ? nullptr : P<u16>(ws, L.hb[t & 1]);
     u16* hb_out = SPLIT ? nullptr : P<u16>(ws, L.hb[(t + 1) & 1]);
     const void* hs = SPLIT ? (const void*)hf_in : (const void*)hb_in;
-    void* XT = tr ? P<void>(ws, L.XT + L.nha * t) : nullptr;
+    void* XT = tr ? P<void>(ws, L.XT + L.nhw * t) : nullptr;
     DISPATCH_VH(c, launch_prop_fwd, PREC, c, hs, P<u16>(adj, AL.Ab), PL, pack, P<void>(ws, L.Xa), XT, s);
-    void* hTo = (tr && t + 1 < c.T) ? P<void>(ws, L.hT + L.nha * (t + 1)) : nullptr;
+    void* hTo = (tr && t + 1 < c.T) ? P<void>(ws, L.hT + L.nhw * (t + 1)) : nullptr;
     float* ro = tr ? P<float>(ws, L.r + L.nh4 * t) : nullptr;
     float* uo = tr ? P<float>(ws, L.u + L.nh4 * t) : nullptr;
     float* co = tr ? P<float>(ws, L.c + L.nh4 * t) : nullptr;
-    void* rhT = tr ? P<void>(ws, L.rhT + L.nha * t) : nullptr;
+    void* rhT = tr ? P<void>(ws, L.rhT + L.nhw * t) : nullptr;
     DISPATCH_HRT(c, launch_gru_fwd, PREC, c, P<void>(ws, L.Xa), hb_in, hf_in, PL, pack, hf_out, hb_out, hTo, ro, uo, co,
                  rhT, s);
   }
@@ -342,9 +343,9 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   for (int t = c.T - 1; t >= 0; --t) {
     DISPATCH_HRT(c, launch_gru_bwd, PREC, c, dA, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
-                 P<void>(ws, L.dzcT + L.nha * t), P<void>(ws, L.dzgT + 2 * L.nha * t), dbc, dbg, s);
+                 P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg, s);
     DISPATCH_VH(c, launch_prop_bwd, PREC, c, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<float>(adj, AL.deg), PL, pack,
-                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nha * t), use_bias ? dbeta : nullptr, s);
+                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? dbeta : nullptr, s);
   }
   {
     Prof p(K_IO, s);
@@ -357,7 +358,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   WgArgs a;
   memset(&a, 0, sizeof(a));
   int np = 0, tiles = 0;
-  const long sa = (long)(L.nha / c.act);  // elements of one [H][N] activation array
+  const long sa = (long)(L.nhw / 2);  // elements of one [H][N] weight-gradient operand array
   auto add = [&](size_t Poff, long stepP, size_t Qoff, long stepQ, float* out, int ldO, int M, int Nn, int nb = 1,
                  long sQb = 0, long sOb = 0) {
     WgProb& p = a.p[np++];
@@ -377,6 +378,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   add(L.rhT, sa, L.dzcT, sa, dWc + H * H, H, H, H);
   // d edge_weights[c] = sum_t h_t^T dM_{c,t}: one problem batched over the C channels
   add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
+  constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
   a.T = c.T;
   int KC = 4096;
@@ -388,8 +390,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const int grid = tiles * a.nchunks;
   {
     Prof p(K_WGRAD, s);
-    if (Prec<PREC>::split || KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, PREC>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad<64, PREC>), dim3(grid), dim3(256), 0, s, a);
+    if (KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, WP>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad<64, WP>), dim3(grid), dim3(256), 0, s, a);
   }
   LAUNCHCHK();
   return GGNN_OK;

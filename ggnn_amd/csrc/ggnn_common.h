@@ -188,6 +188,16 @@ DEV void st_col4(ActT<PREC>* dst, float a, float b, float c, float d) {
   else *(uint2*)dst = make_uint2(pk<Prec<PREC>::f16>(a, b), pk<Prec<PREC>::f16>(c, d));
 }
 
+// Weight-gradient operands (X^T, h^T, (r*h)^T, dzc^T, dzg^T, dM^T) are only
+// summed into the weight gradients, where rounding errors do not compound over
+// timesteps: they are stored as ONE 16-bit limb in every mode (f16 unless the
+// mode is bf16), i.e. the split mode runs k_wgrad with single f16 operands.
+template <int PREC>
+DEV void st_col4w(u16* dst, float a, float b, float c, float d) {
+  *(uint2*)dst = make_uint2(pk<Prec<PREC>::f16>(a, b), pk<Prec<PREC>::f16>(c, d));
+}
+template <int PREC> struct WgradPrec { static constexpr int value = Prec<PREC>::split ? PREC_F16 : PREC; };
+
 // ---- write one accumulator element (value v at row, column e) into image(s)
 template <int PREC, int NCH>
 DEV void img_put(char* hi, char* lo, int row, int e, float v) {

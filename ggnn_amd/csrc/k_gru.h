@@ -23,8 +23,8 @@ __global__ void __launch_bounds__(2 * H)
 k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const float* __restrict__ hf,
           const u16* __restrict__ Wgp, const float* __restrict__ bg, const u16* __restrict__ Wcp,
           const float* __restrict__ bc, long wlo_g, long wlo_c, float* __restrict__ hf_out, u16* __restrict__ hb_out,
-          ActT<PREC>* __restrict__ hT_out, float* __restrict__ r_out, float* __restrict__ u_out,
-          float* __restrict__ c_out, ActT<PREC>* __restrict__ rhT_out, long N) {
+          u16* __restrict__ hT_out, float* __restrict__ r_out, float* __restrict__ u_out,
+          float* __restrict__ c_out, u16* __restrict__ rhT_out, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, NT = 64 * NS, KS = H / 16, R = 32 * RT, HCH = H / 8, KSG = 2 * KS;
   typedef Swz<HCH> SH;
@@ -101,7 +101,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     if (rhT_out) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
+        st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
                        rh[4 * q + 2], rh[4 * q + 3]);
     }
     if (r_out) {
@@ -154,7 +154,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     if (hT_out) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4<PREC>(hT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, ac[rt][4 * q], ac[rt][4 * q + 1],
+        st_col4w<PREC>(hT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, ac[rt][4 * q], ac[rt][4 * q + 1],
                        ac[rt][4 * q + 2], ac[rt][4 * q + 3]);
     }
   }
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(2 * H)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
-          float* __restrict__ dh_out, ActT<PREC>* __restrict__ dzcT, ActT<PREC>* __restrict__ dzgT,
+          float* __restrict__ dh_out, u16* __restrict__ dzcT, u16* __restrict__ dzgT,
           float* __restrict__ dbc, float* __restrict__ dbg, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
@@ -218,7 +218,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         csum += dz[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
       }
-      st_col4<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
+      st_col4w<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
       __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
     }
   }
@@ -268,8 +268,8 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, H + n, zu[i]);
       }
-      st_col4<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
-      st_col4<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
+      st_col4w<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
+      st_col4w<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }

@@ -21,7 +21,7 @@
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, const u16* __restrict__ Wp, long wlo,
-           const float* __restrict__ beta, ActT<PREC>* __restrict__ Xo, ActT<PREC>* __restrict__ XT, int C, long N) {
+           const float* __restrict__ beta, ActT<PREC>* __restrict__ Xo, u16* __restrict__ XT, int C, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KS = H / 16;
@@ -114,7 +114,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     for (int it = 0; it < VT; ++it)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4<PREC>(XT + (long)n * N + rowg + it * 32 + 8 * q + 4 * hh, accx[it][4 * q], accx[it][4 * q + 1],
+        st_col4w<PREC>(XT + (long)n * N + rowg + it * 32 + 8 * q + 4 * hh, accx[it][4 * q], accx[it][4 * q + 1],
                        accx[it][4 * q + 2], accx[it][4 * q + 3]);
   }
   // ---- X row-major through LDS (the h images are free after the last S2)
@@ -151,7 +151,7 @@ template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const float* __restrict__ deg,
            const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
-           ActT<PREC>* __restrict__ dMT, float* __restrict__ dbeta, int C, long N) {
+           u16* __restrict__ dMT, float* __restrict__ dbeta, int C, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
@@ -251,13 +251,10 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       }
       if (dMT) {
         const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
-        const int vm = (int)((((long)ns * 32 + 4 * hh) * N + rowg + j) * sizeof(Act));
+        const int vm = (int)((((long)ns * 32 + 4 * hh) * N + rowg + j) * 2);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int so = (int)(acc_row0(r) * N * sizeof(Act));
-          if constexpr (SPLIT) bst(rdm, am[r], vm, so);
-          else __builtin_amdgcn_raw_buffer_store_b16(to_limb<F16>(am[r]), rdm, vm, so, 0);
-        }
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b16(to_limb<F16>(am[r]), rdm, vm, (int)(acc_row0(r) * N * 2), 0);
       }
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
