@@ -142,9 +142,66 @@ DEV uint4 ld16(const void* p) { return *(const uint4*)p; }
 DEV void st16(void* p, uint4 v) { *(uint4*)p = v; }
 DEV frag lds_frag(const char* img, int off) { return ld16(img + off); }
 
+// LDS-DMA staging of a [R][NCH] tile of 16-byte chunks (row-major in global)
+// into a Swz<NCH> LDS image.  The DMA destination is lane-linear (wave base +
+// 16*lane), so the swizzle goes on the SOURCE address: LDS slot (row, pc)
+// receives logical chunk pc ^ (row & M), the same involution Swz::off reads
+// with.  No VGPR staging; completion is on vmcnt (a __syncthreads drains it).
+template <int NCH, int R, int NT>
+DEV void glds_tile(char* lds, const u16* src, int tid) {
+  typedef Swz<NCH> S;
+  constexpr int TOT = R * NCH;
+  const int lane = tid & 63;
+#pragma unroll
+  for (int p = 0; p < (TOT + NT - 1) / NT; ++p) {
+    const int qb = p * NT + (tid & ~63);  // wave-uniform first slot
+    if (qb < TOT) {
+      const int q = qb + lane, row = q / NCH, pc = q % NCH;
+      __builtin_amdgcn_global_load_lds((const void*)(src + (row * NCH + (pc ^ (row & S::M))) * 8),
+                                       (__attribute__((address_space(3))) void*)(lds + qb * 16), 16, 0, 0);
+    }
+  }
+}
+
 // B-operand fragment of a packed matrix: [strip][kstep][64 lanes][8] limbs
 DEV frag frag_ld(const u16* base, int strip, int ks, int nks, int lane) {
   return ld16(base + ((size_t)(strip * nks + ks) * 64 + lane) * 8);
+}
+
+// ---- software pipeline for B-operand fragments streamed from packed weights
+// (L2-resident): the fragments of k-step ks+D are loaded while k-step ks runs
+// its MFMAs, so each load has D k-steps of MFMA work to hide its L2 latency.
+// The ring is indexed statically (inner loop unrolled by D); the outer loop is
+// kept rolled so the scheduler cannot hoist a whole K sweep of LDS reads into
+// registers.
+struct F2 { frag a, b; };
+struct F4 { frag a, b, c, d; };
+template <int KS, int D, typename LD, typename BODY>
+DEV void b_pipeline(LD&& ld, BODY&& body) {
+  static_assert(KS % D == 0, "k-steps must be a multiple of the pipeline depth");
+  using FB = decltype(ld(0));
+  FB ring[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) ring[p] = ld(p);
+#pragma unroll 1
+  for (int k0 = 0; k0 < KS; k0 += D) {
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+      const int ks = k0 + p;
+      const FB cur = ring[p];
+      if (ks + D < KS) ring[p] = ld(ks + D);
+      body(ks, cur);
+    }
+  }
+}
+
+// The same k loop without the explicit ring (fragments loaded at their k-step;
+// the compiler schedules them): better where the ring's registers would spill
+// or the fully unrolled loop already hides the latency.
+template <int KS, int U, typename LD, typename BODY>
+DEV void b_direct(LD&& ld, BODY&& body) {
+#pragma unroll U
+  for (int ks = 0; ks < KS; ++ks) body(ks, ld(ks));
 }
 
 // Raw buffer access with an SRD built from wave-uniform values: one 32-bit

@@ -51,34 +51,23 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) { ar[rt] = splat(br); au[rt] = splat(bu); }
   }
-  // ---- pass A, x rows of Wg
-#pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
-    const frag wrh = frag_ld(Wgp, ns, ks, KSG, lane), wuh = frag_ld(Wgp, NS + ns, ks, KSG, lane);
-    const frag wrl = SPLIT ? frag_ld(Wgp + wlo_g, ns, ks, KSG, lane) : wrh;
-    const frag wul = SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, ks, KSG, lane) : wuh;
+  // ---- pass A over k in [0, 2H): x rows then h rows of Wg
+  auto ldg = [&](int k) {
+    return F4{frag_ld(Wgp, ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, ns, k, KSG, lane) : frag{},
+              frag_ld(Wgp, NS + ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, k, KSG, lane) : frag{}};
+  };
+  b_pipeline<KSG, 2>(ldg, [&](int k, const F4& w) {
+    const char* ih = (k < KS) ? x_hi : h_hi;
+    const char* il = (k < KS) ? x_lo : h_lo;
+    const int kk = (k < KS) ? k : k - KS;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
-      const frag ah = lds_frag(x_hi, off), al = SPLIT ? lds_frag(x_lo, off) : ah;
-      mma<PREC>(ar[rt], ah, al, wrh, wrl);
-      mma<PREC>(au[rt], ah, al, wuh, wul);
+      const int off = SH::off(rt * 32 + l32, 2 * kk + hh);
+      const frag ah = lds_frag(ih, off), al = SPLIT ? lds_frag(il, off) : ah;
+      mma<PREC>(ar[rt], ah, al, w.a, w.b);
+      mma<PREC>(au[rt], ah, al, w.c, w.d);
     }
-  }
-  // ---- pass A, h rows of Wg
-#pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
-    const frag wrh = frag_ld(Wgp, ns, KS + ks, KSG, lane), wuh = frag_ld(Wgp, NS + ns, KS + ks, KSG, lane);
-    const frag wrl = SPLIT ? frag_ld(Wgp + wlo_g, ns, KS + ks, KSG, lane) : wrh;
-    const frag wul = SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, KS + ks, KSG, lane) : wuh;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
-      const frag ah = lds_frag(h_hi, off), al = SPLIT ? lds_frag(h_lo, off) : ah;
-      mma<PREC>(ar[rt], ah, al, wrh, wrl);
-      mma<PREC>(au[rt], ah, al, wuh, wul);
-    }
-  }
+  });
   const rsrc_t rh_in = mkrsrc(hf + row0 * H, R * H * 4);
   const int vo = (4 * hh * H + n) * 4;
 #pragma unroll
@@ -118,20 +107,20 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) ac[rt] = splat(b0);
   }
-#pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
-    const frag wxh = frag_ld(Wcp, ns, ks, KSG, lane), wrh = frag_ld(Wcp, ns, KS + ks, KSG, lane);
-    const frag wxl = SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : wxh;
-    const frag wrl = SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : wrh;
+  auto ldc = [&](int ks) {
+    return F4{frag_ld(Wcp, ns, ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : frag{},
+              frag_ld(Wcp, ns, KS + ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : frag{}};
+  };
+  b_pipeline<KS, 2>(ldc, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
       const frag xh = lds_frag(x_hi, off), xl = SPLIT ? lds_frag(x_lo, off) : xh;
       const frag qh = lds_frag(h_hi, off), ql = SPLIT ? lds_frag(h_lo, off) : qh;
-      mma<PREC>(ac[rt], xh, xl, wxh, wxl);
-      mma<PREC>(ac[rt], qh, ql, wrh, wrl);
+      mma<PREC>(ac[rt], xh, xl, w.a, w.b);
+      mma<PREC>(ac[rt], qh, ql, w.c, w.d);
     }
-  }
+  });
   // ---- blend + outputs
   const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
   if constexpr (!SPLIT) __syncthreads();  // the h image is reused to stage h' (bf16) below
@@ -230,19 +219,19 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   f32x16 a1[RT], a2[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) { a1[rt] = splat(0.f); a2[rt] = splat(0.f); }
-#pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
-    const frag b1h = frag_ld(WcTp, ns, ks, KS, lane), b2h = frag_ld(WcTp, NS + ns, ks, KS, lane);
-    const frag b1l = SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : b1h;
-    const frag b2l = SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : b2h;
+  auto ld1 = [&](int ks) {
+    return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
+              frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
+  };
+  b_pipeline<KS, 2>(ld1, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      mma<PREC>(a1[rt], ah, al, b1h, b1l);
-      mma<PREC>(a2[rt], ah, al, b2h, b2l);
+      mma<PREC>(a1[rt], ah, al, w.a, w.b);
+      mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
-  }
+  });
   __syncthreads();  // dzc reads done
 
   // ---- phase 2: dh (into a2), dzg
@@ -279,19 +268,19 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   __syncthreads();
 
   // ---- product 2: [dX2 | dh2] = dzg @ Wg^T
-#pragma unroll 2
-  for (int ks = 0; ks < 2 * KS; ++ks) {
-    const frag b1h = frag_ld(WgTp, ns, ks, 2 * KS, lane), b2h = frag_ld(WgTp, NS + ns, ks, 2 * KS, lane);
-    const frag b1l = SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : b1h;
-    const frag b2l = SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : b2h;
+  auto ld2 = [&](int ks) {
+    return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
+              frag_ld(WgTp, NS + ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
+  };
+  b_pipeline<2 * KS, 2>(ld2, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      mma<PREC>(a1[rt], ah, al, b1h, b1l);
-      mma<PREC>(a2[rt], ah, al, b2h, b2l);
+      mma<PREC>(a1[rt], ah, al, w.a, w.b);
+      mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
-  }
+  });
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {

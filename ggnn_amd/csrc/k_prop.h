@@ -13,8 +13,8 @@
 //                                              packed fragments in L2)
 //   AGG: X  += A_c M_c                        (K = V; M_c stays in registers
 //                                              as the B operand, A_c from LDS)
-// LDS: h image(s) [V][H] + one A_c tile [V][V] (register-staged prefetch of
-// A_{c+1} during MT(c)).
+// LDS: h image(s) [V][H] + one A_c tile [V][V] (A_{c+1} staged by LDS-DMA
+// during MT(c+1), after AGG(c) is done with the buffer).
 // Outputs: X [N][H] row-major (GRU operand) and X^T [H][N] (weight-gradient
 // operand, training only).
 // ===========================================================================
@@ -31,7 +31,6 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = V * H * 2;
   constexpr int A_BYTES = V * V * 2;
-  constexpr int APT = (V * ACH + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + A_BYTES];
   char* h_hi = smem;
   char* h_lo = smem + (SPLIT ? IMG : 0);
@@ -44,12 +43,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 
   stage_rows<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
-  uint4 areg[APT];
-#pragma unroll
-  for (int p = 0; p < APT; ++p) {
-    const int q = tid + p * NT;
-    if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), ld16(ag + q * 8));
-  }
+  glds_tile<ACH, V, NT>(abuf, ag, tid);
   __syncthreads();
 
   f32x16 accx[VT];
@@ -57,33 +51,28 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   for (int it = 0; it < VT; ++it) accx[it] = splat(0.f);
 
   for (int c = 0; c < C; ++c) {
-    const bool pre = (c + 1 < C);
-    if (pre) {
-      const u16* an = ag + (long)(c + 1) * V * V;
-#pragma unroll
-      for (int p = 0; p < APT; ++p) {
-        const int q = tid + p * NT;
-        if (q < V * ACH) areg[p] = ld16(an + q * 8);
-      }
-    }
     // ---- MT: M_c[j][n] = sum_k h[j][k] W_c[k][n] + beta_c[n]
     const float bb = beta[c * H + n];
     f32x16 accm[VT];
 #pragma unroll
     for (int rt = 0; rt < VT; ++rt) accm[rt] = splat(bb);
     const u16* wp = Wp + (size_t)c * H * H;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const frag bh = frag_ld(wp, ns, ks, KS, lane);
-      const frag bl = SPLIT ? frag_ld(wp + wlo, ns, ks, KS, lane) : bh;
+    auto ldw = [&](int ks) {
+      return F2{frag_ld(wp, ns, ks, KS, lane), SPLIT ? frag_ld(wp + wlo, ns, ks, KS, lane) : frag{}};
+    };
+    auto mt = [&](int ks, const F2& w) {
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
         const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(h_hi, off);
         const frag al = SPLIT ? lds_frag(h_lo, off) : ah;
-        mma<PREC>(accm[rt], ah, al, bh, bl);
+        mma<PREC>(accm[rt], ah, al, w.a, w.b);
       }
-    }
+    };
+    // measured (config 3): the ring pays in the 3-product split mode, the
+    // fully unrolled direct loop in the single-product modes
+    if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
+    else b_direct<KS, KS>(ldw, mt);
     __syncthreads();  // S1: A_c visible
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
@@ -99,13 +88,8 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
       }
     }
     __syncthreads();  // S2: A_c reads done
-    if (pre) {
-#pragma unroll
-      for (int p = 0; p < APT; ++p) {
-        const int q = tid + p * NT;
-        if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), areg[p]);
-      }
-    }
+    // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
+    if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
   }
 
   // ---- X^T (transposed, weight-gradient operand)
@@ -160,7 +144,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   typedef Swz<ACH> SA;
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = V * H * 2, A_BYTES = V * V * 2;
-  constexpr int APT = (V * ACH + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) char smem[A_BYTES + NIMG * IMG];
   char* abuf = smem;
   char* m_hi = smem + A_BYTES;
@@ -187,12 +170,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   }
 
   const u16* ag = AbT + (long)g * C * V * V;
-  uint4 areg[APT];
-#pragma unroll
-  for (int p = 0; p < APT; ++p) {
-    const int q = tid + p * NT;
-    if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), ld16(ag + q * 8));
-  }
+  glds_tile<ACH, V, NT>(abuf, ag, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
   const int vo = (4 * hh * H + n) * 4;
   f32x16 adh[VT];
@@ -205,15 +183,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   // dM^T store target: element (jt, r) of this lane sits at
   //   dMT + (c*H + ns*32 + 4hh + acc_row0(r)) * N + rowg + jt*32 + l32
   for (int c = 0; c < C; ++c) {
-    const bool pre = (c + 1 < C);
-    if (pre) {
-      const u16* an = ag + (long)(c + 1) * V * V;
-#pragma unroll
-      for (int p = 0; p < APT; ++p) {
-        const int q = tid + p * NT;
-        if (q < V * ACH) areg[p] = ld16(an + q * 8);
-      }
-    }
     if (dbeta) {
       const float* dg = deg + ((long)g * C + c) * V;
       float s = 0.f;
@@ -258,27 +227,21 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       }
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
-    if (pre) {
-#pragma unroll
-      for (int p = 0; p < APT; ++p) {
-        const int q = tid + p * NT;
-        if (q < V * ACH) st16(abuf + SA::off(q / ACH, q % ACH), areg[p]);
-      }
-    }
+    // A_{c+1} lands in LDS by DMA while phase b runs (drained by S2)
+    if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-#pragma unroll 2
-    for (int ks = 0; ks < KS; ++ks) {
-      const frag bh = frag_ld(wt, ns, ks, KS, lane);
-      const frag bl = SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : bh;
+    b_direct<KS, 2>(
+        [&](int ks) { return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}}; },
+        [&](int ks, const F2& w) {
 #pragma unroll
-      for (int jt = 0; jt < VT; ++jt) {
-        const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
-        const frag ah = lds_frag(m_hi, off);
-        const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-        mma<PREC>(adh[jt], ah, al, bh, bl);
-      }
-    }
+          for (int jt = 0; jt < VT; ++jt) {
+            const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
+            const frag ah = lds_frag(m_hi, off);
+            const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
+            mma<PREC>(adh[jt], ah, al, w.a, w.b);
+          }
+        });
     __syncthreads();  // S2: dM image reads done, A_{c+1} staged
   }
   const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
