@@ -176,8 +176,8 @@ def main():
     achieved = fl / (avg_ms * 1e-3) / 1e12 if fl else None
     traffic = None
     tr = load_traffic()
-    if tr and tr.get("kernel") == dom:
-        traffic = tr.get("hbm_bytes_per_launch")
+    if tr and tr.get("precision", "fp32") == args.precision and dom in tr.get("kernels", {}):
+        traffic = tr["kernels"][dom]["hbm_bytes_per_launch"]
     roof = {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / BF16_DENSE_PEAK_TFLOPS) if achieved else None,
             "traffic": traffic, "avg_launch_ms": avg_ms, "algo_flops_per_launch": fl}

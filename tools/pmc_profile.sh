@@ -14,4 +14,4 @@ for grp in \
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pass$i" -o p -- python3 bench.py $ARGS > "$OUT/pass$i.log" 2>&1
 done
-python3 tools/pmc_summary.py "$OUT"
+PMC_BENCH_ARGS="$ARGS" python3 tools/pmc_summary.py "$OUT" "$OUT/pmc_traffic.json"

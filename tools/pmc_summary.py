@@ -1,5 +1,7 @@
 """Aggregate rocprofv3 --pmc CSVs (tools/pmc_profile.sh) per kernel: mean value
-per dispatch of every counter, plus derived rates.  Writes OUT/summary.json."""
+per dispatch of every counter, plus derived rates.  Writes OUT/summary.json and,
+given a second path, the per-launch HBM traffic of the engine's kernel kinds
+(the file bench.py reads for roofline.traffic)."""
 import csv
 import glob
 import json
@@ -45,3 +47,18 @@ for k in sorted(summary):
     print("%-28s " % k[:28] + " ".join("%s=%.3g" % (c, d[c]) for c in (
         "frac_wait_any", "frac_wait_inst", "frac_active", "mfma_busy_per_busy_cycle", "SQ_LDS_BANK_CONFLICT",
         "hbm_read_bytes_corrected", "hbm_write_bytes") if c in d))
+
+if len(sys.argv) > 2:
+    kinds = {}
+    for k, d in summary.items():
+        m = re.match(r"k_(prop_fwd|prop_bwd|gru_fwd|gru_bwd|wgrad)<", k)
+        if m and "hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d:
+            kinds[m.group(1)] = {"kernel": k, "hbm_read_bytes": d["hbm_read_bytes_corrected"],
+                                 "hbm_write_bytes": d["hbm_write_bytes"],
+                                 "hbm_bytes_per_launch": d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]}
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, mean per dispatch; "
+                         "FETCH_SIZE doubled (gfx950 correction, MI355X_MICROARCH.md HBM section)",
+               "bench_args": os.environ.get("PMC_BENCH_ARGS", ""),
+               "precision": (re.findall(r"--precision[= ](\w+)", os.environ.get("PMC_BENCH_ARGS", "")) or ["fp32"])[-1],
+               "kernels": kinds},
+              open(sys.argv[2], "w"), indent=1, sort_keys=True)
