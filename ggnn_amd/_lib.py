@@ -21,7 +21,7 @@ PRECISIONS = ("bf16", "fp16", "fp32")
 EXPORTED = (
     "ggnn_version", "ggnn_last_error", "ggnn_check_dims", "ggnn_workspace_bytes",
     "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
-    "ggnn_forward", "ggnn_backward", "ggnn_kernel_kind_name", "ggnn_profile_begin",
+    "ggnn_forward", "ggnn_backward", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end",
 )
 NUM_KERNEL_KINDS = 8
@@ -29,11 +29,12 @@ NUM_KERNEL_KINDS = 8
 
 class GGNNDims(ctypes.Structure):
     _fields_ = [("b", ctypes.c_int32), ("v", ctypes.c_int32), ("h", ctypes.c_int32),
-                ("C", ctypes.c_int32), ("T", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("C", ctypes.c_int32), ("T", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("edge_keep", ctypes.c_float), ("state_keep", ctypes.c_float), ("seed", ctypes.c_uint64)]
 
     def __repr__(self):
-        return "GGNNDims(b=%d, v=%d, h=%d, C=%d, T=%d, flags=%d)" % (
-            self.b, self.v, self.h, self.C, self.T, self.flags)
+        return "GGNNDims(b=%d, v=%d, h=%d, C=%d, T=%d, flags=%d, edge_keep=%g, state_keep=%g, seed=%d)" % (
+            self.b, self.v, self.h, self.C, self.T, self.flags, self.edge_keep, self.state_keep, self.seed)
 
 
 class GGNNError(RuntimeError):
@@ -79,6 +80,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_forward.argtypes = [_DP, _P, _P, _P, _I, _P, _P, _P]
         lib.ggnn_backward.restype = _I
         lib.ggnn_backward.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+        lib.ggnn_dropout_mask.restype = _I
+        lib.ggnn_dropout_mask.argtypes = [_DP, _I, _I, _P, _P]
         lib.ggnn_kernel_kind_name.restype = ctypes.c_char_p
         lib.ggnn_kernel_kind_name.argtypes = [_I]
         lib.ggnn_profile_begin.restype = _I
@@ -95,11 +98,13 @@ def check(rc: int, what: str) -> None:
         raise GGNNError("%s failed (%d): %s" % (what, rc, msg))
 
 
-def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "bf16") -> GGNNDims:
+def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "bf16",
+         edge_keep: float = 1.0, state_keep: float = 1.0, seed: int = 0) -> GGNNDims:
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s" % (PRECISIONS,))
     flags = (GGNN_USE_EDGE_BIAS if use_edge_bias else 0) | {"bf16": 0, "fp16": GGNN_FP16, "fp32": GGNN_FP32_PARITY}[precision]
-    return GGNNDims(int(b), int(v), int(h), int(C), int(T), flags)
+    return GGNNDims(int(b), int(v), int(h), int(C), int(T), flags, float(edge_keep), float(state_keep),
+                    int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
 def check_dims(d: GGNNDims) -> None:

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -70,7 +71,25 @@ struct Cfg {
   bool split;
   long N;
   int act;  // bytes per stored activation element
+  int vsh;  // log2(V)
+  Drop edrop, sdrop;  // edge-weight / state dropout (thr == 0: off)
+  bool ed, sd;
 };
+
+Drop make_drop(float keep, uint64_t seed) {
+  Drop d;
+  d.k0 = (uint32_t)seed;
+  d.k1 = (uint32_t)(seed >> 32);
+  if (keep >= 1.0f) {
+    d.thr = 0;
+    d.scale = 1.0f;
+  } else {
+    const double t = std::floor((double)keep * 4294967296.0);
+    d.thr = (uint32_t)std::max(1.0, std::min(t, 4294967295.0));
+    d.scale = 1.0f / keep;
+  }
+  return d;
+}
 
 int pad_v(int v) { return v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : -1; }
 
@@ -89,6 +108,14 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   c->split = c->prec == PREC_SPLIT;
   c->act = c->split ? 4 : 2;
   c->N = (long)d->b * V;
+  c->vsh = V == 32 ? 5 : V == 64 ? 6 : 7;
+  if (!(d->edge_keep > 0.0f && d->edge_keep <= 1.0f) || !(d->state_keep > 0.0f && d->state_keep <= 1.0f))
+    return fail(GGNN_EINVAL, "dropout keep probabilities must lie in (0, 1] (edge_keep " +
+                                 std::to_string(d->edge_keep) + ", state_keep " + std::to_string(d->state_keep) + ")");
+  c->edrop = make_drop(d->edge_keep, d->seed);
+  c->sdrop = make_drop(d->state_keep, d->seed);
+  c->ed = c->edrop.thr != 0;
+  c->sd = c->sdrop.thr != 0;
   if ((double)c->N * c->H * 4 >= 2147483647.0) return fail(GGNN_EUNSUP, "b*v*h too large for 32-bit buffer offsets");
   return GGNN_OK;
 }
@@ -96,9 +123,13 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // ---- weight pack: bf16 hi part then lo part of every packed operand
+// Under edge-weight dropout Wf / WT hold one masked copy per timestep
+// (szW bytes apart).
 struct PackL {
-  size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, total;
+  size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, total, szW;
   long loW, loWg, loWc;  // element offset of the lo part from the hi part
+  size_t wf(int t) const { return Wf + (size_t)t * szW; }
+  size_t wt(int t) const { return WT + (size_t)t * szW; }
 };
 PackL pack_layout(const Cfg& c) {
   PackL L;
@@ -107,8 +138,10 @@ PackL pack_layout(const Cfg& c) {
   L.loW = (long)c.C * H * H;
   L.loWg = (long)4 * H * H;
   L.loWc = (long)2 * H * H;
-  L.Wf = o;   o += al(2 * c.C * H * H * 2);
-  L.WT = o;   o += al(2 * c.C * H * H * 2);
+  const int nW = c.ed ? c.T : 1;
+  L.szW = al(2 * c.C * H * H * 2);
+  L.Wf = o;   o += L.szW * nW;
+  L.WT = o;   o += L.szW * nW;
   L.beta = o; o += al(c.C * H * 4);
   L.Wg = o;   o += al(2 * 4 * H * H * 2);
   L.WgT = o;  o += al(2 * 4 * H * H * 2);
@@ -138,7 +171,7 @@ AdjL adj_layout(const Cfg& c) {
 struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
-  size_t dA, dB, dXT, dzcT, dzgT, dMT;
+  size_t dA, dB, dXT, dzcT, dzgT, dMT, G;
   size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
@@ -173,6 +206,7 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.dzcT = o; o += L.nhw * T;
     L.dzgT = o; o += 2 * L.nhw * T;
     L.dMT = o;  o += C * L.nhw * T;
+    if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
   }
   L.total = o;
   return L;
@@ -195,26 +229,27 @@ int gru_rt(const Cfg& c, int maxrt) {
 }
 
 template <int V, int H, int PREC>
-void launch_prop_fwd(const Cfg& c, const void* hs, const u16* Ab, const PackL& PL, const void* pk, void* Xa, void* XT,
-                     hipStream_t s) {
+void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, const PackL& PL, const void* pk, void* Xa,
+                     void* XT, hipStream_t s) {
   Prof p(K_PROP_FWD, s);
   hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab,
-                     P<u16>(pk, PL.Wf), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
+                     P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
 template <int V, int H, int PREC>
-void launch_prop_bwd(const Cfg& c, const void* dXT, const u16* AbT, const float* deg, const PackL& PL, const void* pk,
-                     const float* dh_in, float* dh_out, void* dMT, float* dbeta, hipStream_t s) {
+void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const float* deg, const PackL& PL,
+                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbeta, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
-                     P<u16>(pk, PL.WT), PL.loW, dh_in, dh_out, (u16*)dMT, dbeta, c.C, c.N);
+                     P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbeta, c.C, c.N, c.sdrop, t - 1);
 }
 template <int H, int RT, int PREC>
-void launch_gru_fwd(const Cfg& c, const void* Xa, const u16* hb, const float* hf, const PackL& PL, const void* pk,
-                    float* hf_out, u16* hb_out, void* hT, float* r, float* u, float* cc, void* rhT, hipStream_t s) {
+void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const float* hf, const PackL& PL,
+                    const void* pk, float* hf_out, u16* hb_out, void* hT, float* r, float* u, float* cc, void* rhT,
+                    hipStream_t s) {
   Prof p(K_GRU_FWD, s);
   hipLaunchKernelGGL((k_gru_fwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, (const ActT<PREC>*)Xa, hb,
                      hf, P<u16>(pk, PL.Wg), P<float>(pk, PL.bg), P<u16>(pk, PL.Wc), P<float>(pk, PL.bc), PL.loWg,
-                     PL.loWc, hf_out, hb_out, (u16*)hT, r, u, cc, (u16*)rhT, c.N);
+                     PL.loWc, hf_out, hb_out, (u16*)hT, r, u, cc, (u16*)rhT, c.N, c.sdrop, t, c.vsh);
 }
 template <int H, int RT, int PREC>
 void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
@@ -261,14 +296,17 @@ template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; }
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
 
 void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,
-                 int batch, hipStream_t s) {
+                 int batch, hipStream_t s, Drop dr = Drop{0, 0, 0, 1.0f}, int t = 0) {
   const int total = (N / 32) * (K / 16) * 64;
   Prof p(K_PACK, s);
   if (f16)
-    hipLaunchKernelGGL(k_pack_B<true>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out, sO, lo);
+    hipLaunchKernelGGL(k_pack_B<true>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out,
+                       sO, lo, dr, t);
   else
-    hipLaunchKernelGGL(k_pack_B<false>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out, sO, lo);
+    hipLaunchKernelGGL(k_pack_B<false>, dim3((total + 255) / 256, batch), dim3(256), 0, s, S, ldS, sS, K, N, trans, out,
+                       sO, lo, dr, t);
 }
+const Drop kNoDrop = {0, 0, 0, 1.0f};
 
 // -------------------------------------------------------------------- forward
 template <int PREC>
@@ -284,7 +322,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H, hf0,
-                       SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N, (int)Prec<PREC>::f16);
+                       SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N, (int)Prec<PREC>::f16, kNoDrop, 0);
   }
   if (tr) {
     Prof p(K_IO, s);
@@ -298,14 +336,14 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     u16* hb_out = SPLIT ? nullptr : P<u16>(ws, L.hb[(t + 1) & 1]);
     const void* hs = SPLIT ? (const void*)hf_in : (const void*)hb_in;
     void* XT = tr ? P<void>(ws, L.XT + L.nhw * t) : nullptr;
-    DISPATCH_VH(c, launch_prop_fwd, PREC, c, hs, P<u16>(adj, AL.Ab), PL, pack, P<void>(ws, L.Xa), XT, s);
+    DISPATCH_VH(c, launch_prop_fwd, PREC, c, t, hs, P<u16>(adj, AL.Ab), PL, pack, P<void>(ws, L.Xa), XT, s);
     void* hTo = (tr && t + 1 < c.T) ? P<void>(ws, L.hT + L.nhw * (t + 1)) : nullptr;
     float* ro = tr ? P<float>(ws, L.r + L.nh4 * t) : nullptr;
     float* uo = tr ? P<float>(ws, L.u + L.nh4 * t) : nullptr;
     float* co = tr ? P<float>(ws, L.c + L.nh4 * t) : nullptr;
     void* rhT = tr ? P<void>(ws, L.rhT + L.nhw * t) : nullptr;
-    DISPATCH_HRT(c, launch_gru_fwd, PREC, c, P<void>(ws, L.Xa), hb_in, hf_in, PL, pack, hf_out, hb_out, hTo, ro, uo, co,
-                 rhT, s);
+    DISPATCH_HRT(c, launch_gru_fwd, PREC, c, t, P<void>(ws, L.Xa), hb_in, hf_in, PL, pack, hf_out, hb_out, hTo, ro, uo,
+                 co, rhT, s);
   }
   const float* hfin = tr ? P<float>(ws, L.hfT + L.nh4 * c.T) : P<float>(ws, L.hf[c.T & 1]);
   {
@@ -338,13 +376,14 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   float* dB = P<float>(ws, L.dB);
   {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0);
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
+                       c.sdrop, c.T - 1);
   }
   for (int t = c.T - 1; t >= 0; --t) {
     DISPATCH_HRT(c, launch_gru_bwd, PREC, c, dA, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg, s);
-    DISPATCH_VH(c, launch_prop_bwd, PREC, c, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<float>(adj, AL.deg), PL, pack,
+    DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<float>(adj, AL.deg), PL, pack,
                 dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? dbeta : nullptr, s);
   }
   {
@@ -367,6 +406,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     p.out = out;
     p.ldP = N; p.ldQ = N; p.stepP = stepP; p.stepQ = stepQ; p.sQb = sQb; p.sOb = sOb;
     p.ldO = ldO; p.M = M; p.N = Nn; p.tiles_n = Nn / 128; p.tiles_b = (M / 128) * p.tiles_n;
+    p.sPb = 0; p.pdiv = 1; p.T = c.T;
     p.tile_begin = tiles;
     tiles += nb * p.tiles_b;
   };
@@ -376,11 +416,19 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   // d candidate_kernel: rows [0,H) from X, rows [H,2H) from r*h ; columns dzc (H)
   add(L.XT, sa, L.dzcT, sa, dWc, H, H, H);
   add(L.rhT, sa, L.dzcT, sa, dWc + H * H, H, H, H);
-  // d edge_weights[c] = sum_t h_t^T dM_{c,t}: one problem batched over the C channels
-  add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
+  if (!c.ed) {
+    // d edge_weights[c] = sum_t h_t^T dM_{c,t}: one problem batched over the C channels
+    add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
+  } else {
+    // edge dropout: G[t][c] = h_t^T dM_{c,t} per timestep (batch index t*C + c),
+    // then dW[c] = sum_t mask_t/keep * G[t][c] (k_edge_mask_reduce)
+    HIPCHK(hipMemsetAsync(P<float>(ws, L.G), 0, (size_t)c.T * c.C * H * H * 4, s));
+    add(L.hT, 0, L.dMT, 0, P<float>(ws, L.G), H, H, H, c.T * c.C, sa, (long)H * H);
+    WgProb& q = a.p[np - 1];
+    q.T = 1; q.sPb = sa; q.pdiv = c.C;
+  }
   constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
-  a.T = c.T;
   int KC = 4096;
   while (KC > 32 && (N % KC) != 0) KC /= 2;
   while (KC > 256 && (long)tiles * (N / KC) < 256) KC /= 2;
@@ -392,6 +440,9 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     Prof p(K_WGRAD, s);
     if (KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, WP>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_wgrad<64, WP>), dim3(grid), dim3(256), 0, s, a);
+    if (c.ed)
+      hipLaunchKernelGGL(k_edge_mask_reduce, dim3(grid1d((long)c.C * H * H / 4)), dim3(256), 0, s,
+                         P<const float>(ws, L.G), dW, c.C, c.H, c.T, c.edrop);
   }
   LAUNCHCHK();
   return GGNN_OK;
@@ -404,7 +455,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
 // ===========================================================================
 extern "C" {
 
-int ggnn_version(void) { return 2; }
+int ggnn_version(void) { return 3; }
 const char* ggnn_last_error(void) { return g_err.c_str(); }
 
 const char* ggnn_kernel_kind_name(int kind) {
@@ -486,8 +537,12 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   hipStream_t s = (hipStream_t)stream;
   const PackL L = pack_layout(c);
   const int H = c.H;
-  launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 0, P<u16>(pack, L.Wf), (long)H * H, L.loW, c.C, s);      // MT: Bmat = W_c
-  launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 1, P<u16>(pack, L.WT), (long)H * H, L.loW, c.C, s);      // dh: Bmat = W_c^T
+  for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
+    launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, s,
+                c.edrop, t);  // MT: Bmat = W_c
+    launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, s,
+                c.edrop, t);  // dh: Bmat = W_c^T
+  }
   launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, s);
   launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, s);
   launch_pack(c.prec != PREC_BF16, Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, s);   // Bmat = Wc   [2H][H]
@@ -500,6 +555,21 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
     hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(2 * H)), dim3(256), 0, s, bg, P<float>(pack, L.bg), (long)2 * H);
     hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(H)), dim3(256), 0, s, bc, P<float>(pack, L.bc), (long)H);
   }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!mask) return fail(GGNN_EINVAL, "dropout_mask: NULL pointer");
+  if (kind != 0 && kind != 1) return fail(GGNN_EINVAL, "dropout_mask: kind must be 0 (edge) or 1 (state)");
+  if (t < 0 || t >= c.T) return fail(GGNN_EINVAL, "dropout_mask: t outside [0, T)");
+  hipStream_t s = (hipStream_t)stream;
+  const long total = kind == 0 ? (long)c.C * c.H * c.H : (long)c.b * c.vin * c.H;
+  hipLaunchKernelGGL(k_dropout_mask, dim3(grid1d(total)), dim3(256), 0, s, kind, c.C, c.H, c.b, c.vin, t,
+                     kind == 0 ? c.edrop : c.sdrop, mask);
   LAUNCHCHK();
   return GGNN_OK;
 }

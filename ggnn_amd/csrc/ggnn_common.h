@@ -206,6 +206,39 @@ DEV void b_direct(LD&& ld, BODY&& body) {
 
 // Raw buffer access with an SRD built from wave-uniform values: one 32-bit
 // voffset VGPR per lane, per-element constants in the SGPR soffset.
+// ---- dropout: Philox4x32-10 (Salmon et al., SC'11; Random123 constants)
+// keyed by the 64-bit step seed.  A counter names a group of 4 consecutive
+// rows at one column, and the 4 output words are the 4 rows' draws, which
+// matches the MFMA accumulator layout (4 consecutive rows per register quad):
+//   edge-weight mask, timestep t, W[c][i][j]:  ctr = (i>>2, j, c, t)
+//   state mask,       timestep t, h[g][i][k]:  ctr = (i>>2, k, g, 0x80000000|t)
+// element kept iff word[i&3] < thr, thr = floor(keep * 2^32); kept elements
+// are scaled by 1/keep (tf.nn.dropout: x * (1/keep) * mask).
+struct Drop {
+  uint32_t k0, k1;  // key = seed
+  uint32_t thr;     // 0 = dropout off
+  float scale;      // 1 / keep
+};
+DEV uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+    const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+DEV uint32_t u4_get(const uint4& w, int j) { return j == 0 ? w.x : j == 1 ? w.y : j == 2 ? w.z : w.w; }
+DEV uint4 state_words(const Drop& d, int g, int i, int k, int t) {
+  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)k, (uint32_t)g, 0x80000000u | (uint32_t)t), d.k0, d.k1);
+}
+DEV uint4 edge_words(const Drop& d, int c, int i, int j, int t) {
+  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)c, (uint32_t)t), d.k0, d.k1);
+}
+DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x * d.scale : 0.0f; }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 DEV rsrc_t mkrsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);

@@ -24,7 +24,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
           const u16* __restrict__ Wgp, const float* __restrict__ bg, const u16* __restrict__ Wcp,
           const float* __restrict__ bc, long wlo_g, long wlo_c, float* __restrict__ hf_out, u16* __restrict__ hb_out,
           u16* __restrict__ hT_out, float* __restrict__ r_out, float* __restrict__ u_out,
-          float* __restrict__ c_out, u16* __restrict__ rhT_out, long N) {
+          float* __restrict__ c_out, u16* __restrict__ rhT_out, long N, Drop dr, int t, int vsh) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, NT = 64 * NS, KS = H / 16, R = 32 * RT, HCH = H / 8, KSG = 2 * KS;
   typedef Swz<HCH> SH;
@@ -123,6 +123,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   });
   // ---- blend + outputs
   const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
+  uint4 dw = make_uint4(0, 0, 0, 0);
   if constexpr (!SPLIT) __syncthreads();  // the h image is reused to stage h' (bf16) below
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -131,7 +132,14 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       const int so = (rt * 32 + acc_row0(r)) * H * 4;
       const float cc = tanh_f(ac[rt][r]);
       const float u = au[rt][r];
-      const float hn = u * bld(rh_in, vo, so) + (1.0f - u) * cc;
+      float hn = u * bld(rh_in, vo, so) + (1.0f - u) * cc;
+      if (dr.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
+        if ((r & 3) == 0) {
+          const long grow = row0 + rt * 32 + acc_row0(r) + 4 * hh;
+          dw = state_words(dr, (int)(grow >> vsh), (int)(grow & ((1 << vsh) - 1)), n, t);
+        }
+        hn = drop_apply(dr, u4_get(dw, r & 3), hn);
+      }
       bst(ho, hn, vo, so);
       if (u_out) {
         bst(mkrsrc(u_out + row0 * H, R * H * 4), u, vo, so);

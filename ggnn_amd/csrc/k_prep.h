@@ -7,20 +7,32 @@
 // ldS) into MFMA fragment order [N/32][K/16][64][8] of 16-bit limbs (bf16, or
 // f16 for the split mode), hi part at `out`, lo part (x - limb(x)) at
 // `out + lo_off`.  blockIdx.y selects a matrix of a batch (strides sS / sO).
+// With dr.thr != 0 the source is W[c] (c = blockIdx.y) under the edge-weight
+// dropout mask of timestep t (chem_tensorflow_dense.py:397-403), applied in
+// the reference's element coordinates (i = input row, j = output column) so
+// that the forward pack (Bmat = W_c) and the backward pack (Bmat = W_c^T)
+// see the same mask.
 template <bool F16>
 __global__ void k_pack_B(const float* __restrict__ S, int ldS, long sS, int K, int N, int trans,
-                         u16* __restrict__ out, long sO, long lo_off) {
+                         u16* __restrict__ out, long sO, long lo_off, Drop dr, int t) {
   const int total = (N / 32) * (K / 16) * 64;
   const float* Sb = S + sS * blockIdx.y;
   u16* ob = out + sO * blockIdx.y;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
-    const int lane = q & 63, t = q >> 6;
+    const int lane = q & 63, fi = q >> 6;  // fragment index
     const int nks = K / 16;
-    const int ks = t % nks, strip = t / nks;
+    const int ks = fi % nks, strip = fi / nks;
     const int n = strip * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = trans ? Sb[(long)n * ldS + k0 + j] : Sb[(long)(k0 + j) * ldS + n];
+    if (dr.thr) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int wi = trans ? n : k0 + j, wj = trans ? k0 + j : n;
+        x[j] = drop_apply(dr, u4_get(edge_words(dr, blockIdx.y, wi, wj, t), wi & 3), x[j]);
+      }
+    }
     *(uint4*)(ob + (size_t)q * 8) = pk8<F16>(x);
     *(uint4*)(ob + lo_off + (size_t)q * 8) = pk8_lo<F16>(x);
   }
@@ -66,16 +78,18 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
 }
 
 // h0 [b][vin][H] fp32 -> hf [N][H] fp32 (pad rows zero) and optional hb in
-// the limb format (bf16, or f16 when f16 != 0)
+// the limb format (bf16, or f16 when f16 != 0).  With dr.thr != 0 the state
+// dropout mask of timestep t is applied (backward: dL/dh_T -> dL/dh'_{T-1}).
 __global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H, float* __restrict__ hf,
-                            u16* __restrict__ hb, long N, int f16) {
+                            u16* __restrict__ hb, long N, int f16, Drop dr, int t) {
   const long total = N * H;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const long row = q / H;
     const int col = q % H;
     const long g = row / V;
     const int i = row % V;
-    const float x = (i < vin) ? h0[(g * vin + i) * H + col] : 0.0f;
+    float x = (i < vin) ? h0[(g * vin + i) * H + col] : 0.0f;
+    if (dr.thr) x = drop_apply(dr, u4_get(state_words(dr, (int)g, i, col, t), i & 3), x);
     if (hf) hf[q] = x;
     if (hb) hb[q] = f16 ? to_limb<true>(x) : to_limb<false>(x);
   }
@@ -116,5 +130,45 @@ __global__ void __launch_bounds__(256) k_transpose(const TI* __restrict__ in, TO
       if constexpr (std::is_same<TO, float>::value) out[(long)(c0 + j) * N + r0 + i] = t[i][j];
       else out[(long)(c0 + j) * N + r0 + i] = to_limb<F16>(t[i][j]);
     }
+  }
+}
+
+// d edge_weights under edge dropout: dW[c][i][j] = sum_t mask_t(c,i,j)/keep *
+// G[t][c][i][j], G = the per-timestep h_t^T dM_{c,t} from k_wgrad.  One thread
+// per 4 consecutive rows i (one Philox draw per timestep).
+__global__ void k_edge_mask_reduce(const float* __restrict__ G, float* __restrict__ dW, int C, int H, int T, Drop dr) {
+  const long total = (long)C * (H / 4) * H;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int j = q % H;
+    const int i0 = (int)((q / H) % (H / 4)) * 4;
+    const int c = (int)(q / ((long)H * (H / 4)));
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < T; ++t) {
+      const uint4 w = edge_words(dr, c, i0, j, t);
+      const float* g = G + (((long)t * C + c) * H + i0) * H + j;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += drop_apply(dr, u4_get(w, e), g[(long)e * H]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dW[((long)c * H + i0 + e) * H + j] = s[e];
+  }
+}
+
+// verification: the keep-mask the kernels apply (kind 0: edge [C][H][H] of
+// timestep t; kind 1: state [b][vin][H] of timestep t), 1 = kept
+__global__ void k_dropout_mask(int kind, int C, int H, int b, int vin, int t, Drop dr, uint8_t* __restrict__ m) {
+  const long total = kind == 0 ? (long)C * H * H : (long)b * vin * H;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int k = q % H;
+    const long r = q / H;
+    uint32_t w;
+    if (kind == 0) {
+      const int i = r % H, c = (int)(r / H);
+      w = u4_get(edge_words(dr, c, i, k, t), i & 3);
+    } else {
+      const int i = r % vin, g = (int)(r / vin);
+      w = u4_get(state_words(dr, g, i, k, t), i & 3);
+    }
+    m[q] = (dr.thr == 0 || w < dr.thr) ? 1 : 0;
   }
 }

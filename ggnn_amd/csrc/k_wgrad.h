@@ -16,12 +16,14 @@ struct WgProb {
   float* out;
   long ldP, ldQ, stepP, stepQ;  // elements
   long sQb, sOb;                // batch strides of Q and out (batched problem, e.g. one per channel)
+  long sPb;                     // batch stride of P, applied to (batch index / pdiv)
+  int pdiv, T;                  // T: timesteps summed by this problem
   int ldO, M, N, tiles_n, tiles_b, tile_begin;
 };
 #define WG_MAXP 8
 struct WgArgs {
   WgProb p[WG_MAXP];
-  int nprob, nchunks, KC, T;
+  int nprob, nchunks, KC;
 };
 
 template <int BK, int PREC>
@@ -46,9 +48,9 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
   constexpr int RPB = 256 / (BK * 2);        // tile rows per 256-B LDS bank row
   auto soff = [&](int row, int ch) { return row * BK * 2 + ((ch ^ ((row / RPB) & (CH - 1))) << 4); };
 
-  const int kits = args.KC / BK, nit = kits * args.T;
+  const int kits = args.KC / BK, nit = kits * pr.T;
   const long kbase = (long)chunk * args.KC;
-  const Act* Pb = (const Act*)pr.P;
+  const Act* Pb = (const Act*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
   const Act* Qb = (const Act*)pr.Q + (long)bi * pr.sQb;
   float* const outp = pr.out + (long)bi * pr.sOb;
   // staging registers: one 8-element chunk = 16 B (bf16) or 32 B (fp32)

@@ -41,11 +41,16 @@ def _require(t: torch.Tensor, shape, name: str):
 
 @dataclass
 class WeightPack:
-    """bf16 MFMA-fragment copy of one weight set (see ggnn_pack_weights)."""
+    """MFMA-fragment copy of one weight set (see ggnn_pack_weights).  Under
+    edge-weight dropout (edge_keep < 1) it holds one masked copy per timestep
+    of a T-step pass keyed by `seed`."""
     buf: torch.Tensor
     hidden: int
     channels: int
     use_edge_bias: bool
+    T: int = 1
+    edge_keep: float = 1.0
+    seed: int = 0
 
 
 class PropagationEngine:
@@ -71,27 +76,30 @@ class PropagationEngine:
         self.generation = 0         # bumped by every forward (autograd staleness check)
 
     # ------------------------------------------------------------------ utils
-    def dims(self, b: int, v: int, T: int) -> _lib.GGNNDims:
-        d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision)
+    def dims(self, b: int, v: int, T: int, edge_keep: float = 1.0, state_keep: float = 1.0,
+             seed: int = 0) -> _lib.GGNNDims:
+        d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision, edge_keep, state_keep, seed)
         _lib.check_dims(d)
         return d
 
-    def workspace(self, b: int, v: int, T: int, training: bool) -> torch.Tensor:
-        key = (b, v, T, bool(training))
+    def workspace(self, b: int, v: int, T: int, training: bool, edge_dropout: bool = False) -> torch.Tensor:
+        key = (b, v, T, bool(training), bool(edge_dropout))
         ws = self._ws.get(key)
         if ws is None:
             if len(self._ws) >= 4:      # keep a handful of shapes (bucketed batches)
                 self._ws.clear()
-            ws = torch.empty(_lib.workspace_bytes(self.dims(b, v, T), training),
-                             dtype=torch.uint8, device=self.device)
+            d = self.dims(b, v, T, edge_keep=0.5 if edge_dropout else 1.0)
+            ws = torch.empty(_lib.workspace_bytes(d, training), dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
         return ws
 
     # ---------------------------------------------------------------- weights
-    def pack_weights(self, weights: dict) -> WeightPack:
+    def pack_weights(self, weights: dict, T: int = 1, edge_keep: float = 1.0, seed: int = 0) -> WeightPack:
         """weights: dict of fp32 device tensors with the reference's shapes:
         edge_weights [C,h,h], edge_biases [C,1,h] (or [C,h]), gates_kernel [2h,2h],
-        gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h]."""
+        gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h].
+        edge_keep < 1: edge-weight dropout (chem_tensorflow_dense.py:397-403),
+        one fresh mask per timestep of a T-step pass, keyed by seed."""
         h, C = self.h, self.C
         _require(weights["edge_weights"], (C, h, h), "edge_weights")
         eb = weights.get("edge_biases") if self.use_edge_bias else None
@@ -103,14 +111,15 @@ class PropagationEngine:
         _require(weights["gates_bias"], (2 * h,), "gates_bias")
         _require(weights["candidate_kernel"], (2 * h, h), "candidate_kernel")
         _require(weights["candidate_bias"], (h,), "candidate_bias")
-        d = self.dims(1, 1, 1)
+        T = int(T) if edge_keep < 1.0 else 1
+        d = self.dims(1, 1, T, edge_keep=edge_keep, seed=seed)
         buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)
         _lib.check(self._lib.ggnn_pack_weights(
             ctypes.byref(d), _ptr(buf), _ptr(weights["edge_weights"]), _ptr(eb),
             _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
             _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream()),
             "ggnn_pack_weights")
-        return WeightPack(buf, h, C, self.use_edge_bias)
+        return WeightPack(buf, h, C, self.use_edge_bias, T, float(edge_keep), int(seed))
 
     # -------------------------------------------------------------- adjacency
     def set_adjacency(self, adjacency: torch.Tensor) -> None:
@@ -135,19 +144,25 @@ class PropagationEngine:
 
     # ---------------------------------------------------------------- compute
     def forward(self, h0: torch.Tensor, pack: WeightPack, T: int, training: bool = False,
-                out: torch.Tensor | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, state_keep: float = 1.0) -> torch.Tensor:
+        """state_keep < 1: GRU state dropout (DropoutWrapper, chem_tensorflow_dense.py:239-240),
+        keyed by the pack's seed; edge-weight dropout comes with the pack."""
         if self._batch is None:
             raise RuntimeError("set_adjacency() must be called before forward()")
+        if not isinstance(pack, WeightPack):
+            raise RuntimeError("forward() needs a WeightPack from pack_weights()")
         b, v = self._batch
         _require(h0, (b, v, self.h), "initial_node_representations")
-        ws = self.workspace(b, v, T, training)
-        d = self.dims(b, v, T)
+        if pack.edge_keep < 1.0 and pack.T != T:
+            raise ValueError("the pack holds edge-dropout masks for T=%d, forward asked for T=%d" % (pack.T, T))
+        ws = self.workspace(b, v, T, training, pack.edge_keep < 1.0)
+        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed)
         if out is None:
             out = torch.empty((b, v, self.h), dtype=torch.float32, device=self.device)
         _require(out, (b, v, self.h), "out")
         _lib.check(self._lib.ggnn_forward(ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws),
                                           int(bool(training)), _ptr(h0), _ptr(out), _stream()), "ggnn_forward")
-        self._trained = (b, v, T, pack, ws) if training else None
+        self._trained = (b, v, T, pack, ws, float(state_keep)) if training else None
         self.generation += 1
         return out
 
@@ -168,14 +183,24 @@ class PropagationEngine:
         the six weight gradients (reference shapes, fp32)."""
         if self._trained is None:
             raise RuntimeError("backward() needs a preceding forward(..., training=True) on this batch")
-        b, v, T, pack, ws = self._trained
+        b, v, T, pack, ws, state_keep = self._trained
         _require(dhT, (b, v, self.h), "dL/dh_T")
         if grads is None:
             grads = self.alloc_grads(b, v)
-        d = self.dims(b, v, T)
+        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed)
         _lib.check(self._lib.ggnn_backward(
             ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws), _ptr(dhT), _ptr(grads["h0"]),
             _ptr(grads["edge_weights"]), _ptr(grads.get("edge_biases")), _ptr(grads["gates_kernel"]),
             _ptr(grads["gates_bias"]), _ptr(grads["candidate_kernel"]), _ptr(grads["candidate_bias"]),
             _stream()), "ggnn_backward")
         return grads
+
+    def dropout_mask(self, kind: str, b: int, v: int, T: int, t: int, keep: float, seed: int) -> torch.Tensor:
+        """The keep-mask (uint8, 1 = kept) the kernels apply: kind "edge" ->
+        [C, h, h] of timestep t; kind "state" -> [b, v, h] of timestep t."""
+        k = {"edge": 0, "state": 1}[kind]
+        d = self.dims(b, v, T, keep if k == 0 else 1.0, keep if k == 1 else 1.0, seed)
+        shape = (self.C, self.h, self.h) if k == 0 else (b, v, self.h)
+        m = torch.empty(shape, dtype=torch.uint8, device=self.device)
+        _lib.check(self._lib.ggnn_dropout_mask(ctypes.byref(d), k, int(t), _ptr(m), _stream()), "ggnn_dropout_mask")
+        return m

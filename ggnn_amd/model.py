@@ -41,14 +41,14 @@ class _Propagate(torch.autograd.Function):
     """h_T = GGNN_T(h0; W, beta, GRU) through the HIP engine."""
 
     @staticmethod
-    def forward(ctx, h0, W, beta, Wg, bg, Wc, bc, engine, T):
+    def forward(ctx, h0, W, beta, Wg, bg, Wc, bc, engine, T, edge_keep=1.0, state_keep=1.0, seed=0):
         weights = {"edge_weights": W.contiguous(), "edge_biases": beta.contiguous() if beta is not None else None,
                    "gates_kernel": Wg.contiguous(), "gates_bias": bg.contiguous(),
                    "candidate_kernel": Wc.contiguous(), "candidate_bias": bc.contiguous()}
-        pack = engine.pack_weights(weights)
+        pack = engine.pack_weights(weights, T=T, edge_keep=edge_keep, seed=seed)
         # (autograd runs Function.forward with grad mode off: ask the ctx)
         training = any(ctx.needs_input_grad[:7])
-        out = engine.forward(h0.contiguous(), pack, T, training=training)
+        out = engine.forward(h0.contiguous(), pack, T, training=training, state_keep=state_keep)
         ctx.engine = engine
         ctx.generation = engine.generation
         ctx.has_beta = beta is not None
@@ -67,7 +67,7 @@ class _Propagate(torch.autograd.Function):
         if ctx.has_beta and db is not None:
             db = db.view(ctx.beta_shape)
         return (g["h0"], g["edge_weights"], db if ctx.has_beta else None, g["gates_kernel"], g["gates_bias"],
-                g["candidate_kernel"], g["candidate_bias"], None, None)
+                g["candidate_kernel"], g["candidate_bias"], None, None, None, None, None)
 
 
 class DenseGGNNChemModel(BtbBatching):
@@ -188,7 +188,13 @@ class DenseGGNNChemModel(BtbBatching):
         eng = self._engine("main" if fixed_ts is None else "fixed")
         eng.set_adjacency(self.placeholders["adjacency_matrix"])
         gru = self.weights["node_gru"]
+        # dropout as fed (chem_tensorflow_dense.py:860-861 training, :938-940 eval);
+        # a fresh Philox seed per call = fresh masks per step, like TF's stateful RNG
+        edge_keep = float(self.placeholders.get("edge_weight_dropout_keep_prob", 1.0))
+        state_keep = float(self.placeholders.get("graph_state_keep_prob", 1.0))
+        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
         out = _Propagate.apply(h0, W, beta, gru["gates_kernel"], gru["gates_bias"],
-                               gru["candidate_kernel"], gru["candidate_bias"], eng, T)
+                               gru["candidate_kernel"], gru["candidate_bias"], eng, T, edge_keep, state_keep, seed)
+        self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=seed)
         self.ops["final_node_representations" if fixed_ts is None else "second_node_representations"] = out
         return out

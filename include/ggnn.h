@@ -19,6 +19,9 @@
  *                          (:391-437) + GRUCell (:333), returns [b, v, h]
  *   ggnn_backward       <- TF autodiff of the same loop (chem_tensorflow.py:496):
  *                          dL/dh0 and the weight gradients (before clip/Adam)
+ *   ggnn_dims.edge_keep / state_keep / seed
+ *                       <- tf.nn.dropout of the edge weights (:397-403) and the
+ *                          GRUCell DropoutWrapper (:239-240), fed at :860-861
  *
  * Conventions
  *  - Every tensor argument is a raw device pointer (hipMalloc'd or any HIP
@@ -77,6 +80,18 @@ typedef struct ggnn_dims {
   int32_t C;     /* adjacency channels = 2 * num_edge_types                 */
   int32_t T;     /* timesteps (params['num_timesteps'] or fixed_ts)         */
   int32_t flags; /* GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY or GGNN_FP16      */
+  /* Dropout (applied whenever keep < 1, as the reference applies it whenever
+   * a keep probability < 1 is fed; it feeds 1.0 at evaluation, :938-940):
+   *   edge_keep  = placeholders['edge_weight_dropout_keep_prob']: every
+   *                timestep multiplies W by a fresh mask / keep (:397-403);
+   *   state_keep = placeholders['graph_state_keep_prob']: DropoutWrapper
+   *                state dropout of every new GRU state (:239-240).
+   * Both must lie in (0, 1].  Masks are Philox4x32-10 keyed by `seed`
+   * (DESIGN.md "Dropout"), so pack, forward and backward of one step must
+   * see the same seed; draw a new seed per training step. */
+  float edge_keep;
+  float state_keep;
+  uint64_t seed;
 } ggnn_dims;
 
 int ggnn_version(void);
@@ -121,6 +136,11 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
                   float* d_gates_kernel, float* d_gates_bias,
                   float* d_candidate_kernel, float* d_candidate_bias,
                   ggnn_stream_t stream);
+
+/* Materialise a dropout keep-mask (1 = kept, 0 = dropped) exactly as the
+ * kernels apply it, for verification: kind 0 = edge-weight mask of timestep t
+ * ([C][h][h] bytes), kind 1 = state mask of timestep t ([b][v][h] bytes). */
+int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_stream_t stream);
 
 /* Optional per-kernel timing (HIP events around every launch of the library
  * on the launch's stream), used by bench.py for the roofline.  Not for use

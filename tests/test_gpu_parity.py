@@ -256,3 +256,99 @@ def test_drop_in_model_on_reference_dev_batches():
         assert _nmax(h0_t.grad.cpu().numpy(), gref["h0"]) <= FP32_TOL
         assert _nmax(m.weights["edge_weights"].grad.cpu().numpy(), gref["edge_weights"]) <= FP32_TOL
         assert _nmax(m.weights["node_gru"]["gates_kernel"].grad.cpu().numpy(), gref["gates_kernel"]) <= FP32_TOL
+
+
+# ------------------------------------------------------------------ dropout
+@pytest.mark.parametrize("b,v,h,C,T,t", [(3, 21, 128, 4, 3, 0), (2, 128, 256, 8, 5, 4), (5, 50, 64, 6, 2, 1)])
+def test_dropout_masks_bit_exact(b, v, h, C, T, t):
+    """The keep-masks the kernels apply equal the oracle's Philox restatement
+    bit for bit (integer work: exact)."""
+    _torch()
+    from ggnn_amd.engine import PropagationEngine
+    eng = PropagationEngine(h, C, precision="fp32")
+    seed = 0x1234_5678_9ABC + t
+    for keep in (0.9, 0.5):
+        me = eng.dropout_mask("edge", b, v, T, t, keep, seed).cpu().numpy().astype(bool)
+        assert np.array_equal(me, O.edge_keep_mask(C, h, t, keep, seed))
+        ms = eng.dropout_mask("state", b, v, T, t, keep, seed).cpu().numpy().astype(bool)
+        assert np.array_equal(ms, O.state_keep_mask(b, v, h, t, keep, seed))
+    assert eng.dropout_mask("state", b, v, T, t, 1.0, seed).cpu().numpy().all()
+
+
+def _run_dropout(A, h0, w, T, precision, dr, dhT):
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    b, C, v, _ = A.shape
+    eng = PropagationEngine(h0.shape[-1], C, precision=precision)
+    dev = eng.device
+    pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()},
+                            T=T, edge_keep=dr["edge_keep"], seed=dr["seed"])
+    eng.set_adjacency(torch.from_numpy(np.ascontiguousarray(A)).to(dev))
+    out = eng.forward(torch.from_numpy(np.ascontiguousarray(h0)).to(dev), pack, T, training=True,
+                      state_keep=dr["state_keep"])
+    g = eng.backward(torch.from_numpy(np.ascontiguousarray(dhT)).to(dev))
+    res = {"hT": out.cpu().numpy()}
+    res.update({k: (None if x is None else x.cpu().numpy()) for k, x in g.items()})
+    return res
+
+
+@pytest.mark.parametrize("b,v,h,C,T,ek,sk", [
+    (3, 20, 128, 4, 3, 0.9, 0.9),      # the reference's training feed (keep 0.9 for both, :860-861)
+    (2, 128, 256, 8, 3, 0.9, 0.9),
+    (4, 50, 256, 6, 2, 1.0, 0.7),      # state dropout only
+    (4, 50, 128, 6, 2, 0.6, 1.0),      # edge dropout only
+])
+def test_dropout_fp32_parity(b, v, h, C, T, ek, sk):
+    A, h0, w = _case(b, v, h, C, seed=b * 3 + v)
+    dhT = np.random.default_rng(8).standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=ek, state_keep=sk, seed=987654321 + T)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run_dropout(A, h0, w, T, "fp32", dr, dhT)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+    # dropout is really on: the same step without it differs by O(1)
+    nodrop, _ = O.forward(A64, h0.astype(np.float64), w64, T, keep_cache=False)
+    assert np.abs(nodrop - ref).max() > 0.05
+
+
+def test_dropout_bf16_statistical():
+    b, v, h, C, T = 4, 64, 256, 8, 3
+    A, h0, w = _case(b, v, h, C, seed=5)
+    dhT = np.random.default_rng(9).standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=0.9, state_keep=0.9, seed=42)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run_dropout(A, h0, w, T, "bf16", dr, dhT)
+    assert _nrms(got["hT"], ref) <= BF16_RMS_CAP
+    for k in GRADS:
+        assert _nrms(got[k].reshape(gref[k].shape), gref[k]) <= 5 * BF16_RMS_TOL, k
+
+
+def test_drop_in_model_training_feed_applies_dropout():
+    """make_minibatch_iterator(is_training=True) feeds keep = 0.9 for both
+    dropouts (chem_tensorflow_dense.py:860-861): the model's output must equal
+    the oracle with the Philox masks of the seed it drew."""
+    torch = _torch()
+    from ggnn_amd.model import DenseGGNNChemModel
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
+    data = json.loads(str(g["raw_json"]))
+    m = DenseGGNNChemModel(params={"hidden_size": 128, "num_timesteps": 2, "batch_size": 8},
+                           num_edge_types=int(g["num_edge_types"]), output_size_edges=int(g["output_size_edges"]),
+                           pos_size=int(g["pos_size"]), bucket_max_nodes=int(g["bucket_max_nodes"]),
+                           precision="fp32")
+    fd = next(iter(m.make_minibatch_iterator(m.process_raw_graphs(data[:16], True), True)))
+    assert fd["graph_state_keep_prob"] == 0.9 and fd["edge_weight_dropout_keep_prob"] == 0.9
+    m.feed(fd)
+    b, v = fd["num_graphs"], fd["num_vertices"]
+    h0 = np.random.default_rng(1).uniform(-0.5, 0.5, (b, v, 128)).astype(np.float32)
+    out = m.compute_final_node_representations(torch.from_numpy(h0).to(m.device))
+    w64 = {"edge_weights": m.weights["edge_weights"].detach().cpu().numpy().astype(np.float64),
+           "edge_biases": m.weights["edge_biases"].detach().cpu().numpy().astype(np.float64)}
+    w64.update({k: t.detach().cpu().numpy().astype(np.float64) for k, t in m.weights["node_gru"].items()})
+    ref, _ = O.forward(np.asarray(fd["adjacency_matrix"], np.float64), h0.astype(np.float64), w64, 2,
+                       keep_cache=False, dropout=m.last_dropout)
+    assert np.abs(out.detach().cpu().numpy() - ref).max() <= FP32_TOL

@@ -61,3 +61,22 @@ def test_null_pointers_are_rejected_without_gpu(lib):
     d = _lib.dims(2, 16, 128, 4, 2)
     rc = lib.ggnn_forward(ctypes.byref(d), None, None, None, 0, None, None, None)
     assert rc == -1 and b"NULL" in lib.ggnn_last_error()
+
+
+def test_dropout_dims_validation_and_sizes(lib):
+    """Keep probabilities must lie in (0, 1]; edge dropout holds one masked
+    weight copy per timestep in the pack and a per-timestep dW scratch."""
+    import ctypes
+    from ggnn_amd import _lib
+    for ek, sk in ((0.0, 1.0), (1.0, 0.0), (1.5, 1.0), (1.0, -0.1), (float("nan"), 1.0)):
+        d = _lib.dims(2, 16, 128, 4, 3, edge_keep=ek, state_keep=sk)
+        assert lib.ggnn_check_dims(ctypes.byref(d)) == -1
+        assert b"keep" in lib.ggnn_last_error()
+    d1 = _lib.dims(256, 128, 256, 8, 5)
+    d2 = _lib.dims(256, 128, 256, 8, 5, edge_keep=0.9, state_keep=0.9, seed=3)
+    d3 = _lib.dims(256, 128, 256, 8, 5, edge_keep=1.0, state_keep=0.9, seed=3)
+    p1, p2 = _lib.weight_pack_bytes(d1), _lib.weight_pack_bytes(d2)
+    assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2)       # (T-1) extra masked copies of W and W^T
+    assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
+    assert _lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True) == 5 * 8 * 256 * 256 * 4
+    assert _lib.workspace_bytes(d2, False) == _lib.workspace_bytes(d1, False)

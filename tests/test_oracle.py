@@ -109,3 +109,70 @@ def test_adjacency_semantics_match_reference_test_vectors():
     assert A[2, 3, 1] == 1 and A[2, 3, 2] == 1 and A[3, 0, 3] == 1      # outgoing (transposed)
     assert A[3, 0, 1] == 1 and A[3, 1, 2] == 1 and A[3, 2, 3] == 1      # next-word edges
     assert A.sum() == 12
+
+
+# ---------------------------------------------------------------- dropout
+def test_philox_known_answer_vectors():
+    """Random123's published Philox4x32-10 known-answer vectors (kat_vectors)."""
+    kats = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+            ((0xffffffff,) * 4, (0xffffffff, 0xffffffff), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+            ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+             (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, exp in kats:
+        assert tuple(int(x) for x in O.philox4x32_10(*ctr, key)) == exp
+
+
+def test_dropout_masks_fresh_per_step_and_seeded():
+    m0 = O.edge_keep_mask(4, 64, 0, 0.9, seed=7)
+    m1 = O.edge_keep_mask(4, 64, 1, 0.9, seed=7)
+    assert m0.shape == (4, 64, 64) and abs(m0.mean() - 0.9) < 0.01
+    assert (m0 != m1).mean() > 0.1                               # fresh mask per timestep (:397-403)
+    assert np.array_equal(m0, O.edge_keep_mask(4, 64, 0, 0.9, seed=7))
+    assert (m0 != O.edge_keep_mask(4, 64, 0, 0.9, seed=8)).mean() > 0.1
+    s = O.state_keep_mask(5, 23, 64, 3, 0.5, seed=1)
+    assert s.shape == (5, 23, 64) and abs(s.mean() - 0.5) < 0.02
+    # a graph's mask does not depend on the batch it sits in (counter = (i>>2, k, g, t))
+    assert np.array_equal(O.state_keep_mask(7, 23, 64, 3, 0.5, seed=1)[:5], s)
+
+
+def test_dropout_forward_semantics():
+    """W_t = W * mask_t / keep (edge) and h = GRU(...) * mask_t / keep (state)."""
+    A, h0 = O.synthetic_batch(2, 6, 8, 4, seed=2, density=0.4, dtype=np.float64)
+    w = {k: v.astype(np.float64) for k, v in O.synthetic_weights(8, 4, seed=1).items()}
+    dr = dict(edge_keep=0.75, state_keep=0.6, seed=99)
+    hT, _ = O.forward(A, h0, w, 2, dropout=dr)
+    h = h0
+    for t in range(2):
+        em = O.edge_keep_mask(4, 8, t, 0.75, 99)
+        X = O.message_aggregate_fast(A, h, w["edge_weights"] * em / 0.75, w["edge_biases"])
+        hn, _ = O.gru_cell(X.reshape(-1, 8), h.reshape(-1, 8), w["gates_kernel"], w["gates_bias"],
+                           w["candidate_kernel"], w["candidate_bias"])
+        h = hn.reshape(h.shape) * O.state_keep_mask(2, 6, 8, t, 0.6, 99) / 0.6
+    np.testing.assert_allclose(hT, h, rtol=1e-12, atol=1e-12)
+
+
+def test_dropout_backward_matches_finite_differences():
+    A, h0 = O.synthetic_batch(2, 5, 4, 4, seed=3, density=0.4, dtype=np.float64)
+    w = {k: v.astype(np.float64) for k, v in O.synthetic_weights(4, 4, seed=1).items()}
+    dr = dict(edge_keep=0.7, state_keep=0.8, seed=12345)
+    T = 2
+    hT, caches = O.forward(A, h0, w, T, dropout=dr)
+    dhT = np.random.default_rng(0).standard_normal(hT.shape)
+    g = O.backward(A, dhT, caches, w)
+
+    def loss(w_, h0_):
+        return float((O.forward(A, h0_, w_, T, keep_cache=False, dropout=dr)[0] * dhT).sum())
+
+    eps = 1e-6
+    for key in ("h0", "edge_weights", "edge_biases", "gates_kernel", "candidate_bias"):
+        base = h0 if key == "h0" else w[key]
+        num = np.zeros_like(base)
+        for idx in np.ndindex(base.shape):
+            p, m = base.copy(), base.copy()
+            p[idx] += eps
+            m[idx] -= eps
+            if key == "h0":
+                num[idx] = (loss(w, p) - loss(w, m)) / (2 * eps)
+            else:
+                num[idx] = (loss({**w, key: p}, h0) - loss({**w, key: m}, h0)) / (2 * eps)
+        assert np.abs(num - g[key]).max() <= 1e-7 * max(1.0, np.abs(num).max()), key
