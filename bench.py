@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropout-keep", type=float, default=0.9,
+                    help="keep probability of the dropout-on line (graph_state_dropout_keep_prob)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
                     help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
@@ -138,10 +140,15 @@ def main():
     gviews["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
     out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
 
-    def step():
-        pack = eng.pack_weights(w_d)
+    nstep = [0]
+
+    def step(keep=1.0):
+        # keep < 1: the reference's training feed (edge-weight + state dropout,
+        # chem_tensorflow_dense.py:860-861), a fresh Philox seed every step
+        nstep[0] += 1
+        pack = eng.pack_weights(w_d, T=T, edge_keep=keep, seed=nstep[0])
         eng.set_adjacency(A_d)
-        eng.forward(h0_d, pack, T, training=True, out=out)
+        eng.forward(h0_d, pack, T, training=True, out=out, state_keep=keep)
         eng.backward(dhT, gviews)
         grads.all_reduce()
 
@@ -153,19 +160,38 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    # timed region: exactly K steps, nothing else on the stream
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    dt = (t1 - t0) / args.steps
+    # the same K steps again with a HIP event pair around every library launch
+    # (kernel durations for the roofline; the events add gaps between launches,
+    # so this pass is not the headline time)
     timer = _lib.KernelTimer(max_launches=200 * max(args.steps, 1))
     with timer:
         barrier()
-        t0 = time.perf_counter()
+        t3 = time.perf_counter()
         for _ in range(args.steps):
             step()
         barrier()
-        t1 = time.perf_counter()
-    dt = (t1 - t0) / args.steps
+        dt_instr = (time.perf_counter() - t3) / args.steps
+    # the same step with the training-feed dropout (keep 0.9 for both), reported beside
+    for _ in range(args.warmup):
+        step(args.dropout_keep)
+    barrier()
+    t2 = time.perf_counter()
+    for _ in range(args.steps):
+        step(args.dropout_keep)
+    barrier()
+    dt_drop = (time.perf_counter() - t2) / args.steps
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt, dt_drop], dtype=torch.float64, device=dev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        dt = float(tt.item())
+        dt, dt_drop = float(tt[0].item()), float(tt[1].item())
 
     # roofline of the dominant kernel (largest total time in the timed region)
     kinds = {k: ms for k, ms in timer.total_ms.items() if timer.launches.get(k)}
@@ -209,6 +235,11 @@ def main():
             "roofline": roof,
             "achieved_step_tflops": world * b * fpg / dt / 1e12,
             "kernel_breakdown": breakdown,
+            "ms_per_step_event_instrumented": dt_instr * 1e3,
+            "dropout_on": {"edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
+                           "value": world * b / dt_drop, "ms_per_step": dt_drop * 1e3,
+                           "note": "same step with the reference's training-feed dropout (:860-861); "
+                                   "value above is dropout off (keep 1, the parity setting)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
