@@ -162,7 +162,7 @@ AdjL adj_layout(const Cfg& c) {
   size_t o = 0;
   L.Ab = o;  o += al((size_t)c.b * c.C * c.V * c.V * 2);
   L.AbT = o; o += al((size_t)c.b * c.C * c.V * c.V * 2);
-  L.deg = o; o += al((size_t)c.b * c.C * c.V * 4);
+  L.deg = o; o += al((size_t)c.b * c.C * c.V * 2);
   L.total = o;
   return L;
 }
@@ -171,7 +171,7 @@ AdjL adj_layout(const Cfg& c) {
 struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
-  size_t dA, dB, dXT, dzcT, dzgT, dMT, G;
+  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp;
   size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
@@ -207,6 +207,7 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.dzgT = o; o += 2 * L.nhw * T;
     L.dMT = o;  o += C * L.nhw * T;
     if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
+    L.dbp = o; o += al(T * (size_t)c.b * C * H * 4);    // per-(timestep, graph) dL/dbeta partials
   }
   L.total = o;
   return L;
@@ -236,11 +237,11 @@ void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, const P
                      P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
 template <int V, int H, int PREC>
-void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const float* deg, const PackL& PL,
-                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbeta, hipStream_t s) {
+void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, const PackL& PL,
+                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
-                     P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbeta, c.C, c.N, c.sdrop, t - 1);
+                     P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1);
 }
 template <int H, int RT, int PREC>
 void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const float* hf, const PackL& PL,
@@ -366,12 +367,12 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
 
   HIPCHK(hipMemsetAsync(dW, 0, (size_t)c.C * H * H * 4, s));
-  if (use_bias) HIPCHK(hipMemsetAsync(dbeta, 0, (size_t)c.C * H * 4, s));
   HIPCHK(hipMemsetAsync(dWg, 0, (size_t)4 * H * H * 4, s));
   HIPCHK(hipMemsetAsync(dbg, 0, (size_t)2 * H * 4, s));
   HIPCHK(hipMemsetAsync(dWc, 0, (size_t)2 * H * H * 4, s));
   HIPCHK(hipMemsetAsync(dbc, 0, (size_t)H * 4, s));
 
+  if (use_bias) HIPCHK(hipMemsetAsync(dbeta, 0, (size_t)c.C * H * 4, s));
   float* dA = P<float>(ws, L.dA);
   float* dB = P<float>(ws, L.dB);
   {
@@ -383,13 +384,16 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     DISPATCH_HRT(c, launch_gru_bwd, PREC, c, dA, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg, s);
-    DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<float>(adj, AL.deg), PL, pack,
-                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? dbeta : nullptr, s);
+    DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg), PL, pack,
+                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr, s);
   }
   {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
                        (long)c.b);
+    if (use_bias)
+      hipLaunchKernelGGL(k_sum_graphs, dim3(grid1d((long)c.C * H, 64), 64), dim3(64), 0, s, P<const float>(ws, L.dbp),
+                         dbeta, c.T * c.b, (long)c.C * H);
   }
 
   // weight gradients: out[m][n] += sum_{t,rows} P_t[m][row] Q_t[n][row]
@@ -585,7 +589,7 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
   Prof p(K_ADJ, s);
 #define PREP_ADJ(VV, F)                                                                                       \
   hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT), \
-                     P<float>(adj, L.deg))
+                     P<u16>(adj, L.deg))
   if (c.prec != PREC_BF16) {
     if (c.V == 32) PREP_ADJ(32, true);
     else if (c.V == 64) PREP_ADJ(64, true);

@@ -34,6 +34,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // an MFMA A/B operand fragment: 8 x 16-bit (bf16 or f16 limbs)
 typedef uint4 frag;
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 
 #define DEV __device__ __forceinline__
 
@@ -206,6 +207,28 @@ DEV void b_direct(LD&& ld, BODY&& body) {
 
 // Raw buffer access with an SRD built from wave-uniform values: one 32-bit
 // voffset VGPR per lane, per-element constants in the SGPR soffset.
+// 4x4 transpose of 16-bit values inside each lane quad.  Lane L (= lane & 3)
+// holds column L of a 4-row block: P0 = rows (0,1), P1 = rows (2,3), low half
+// first.  Returns row L's 4 columns (column 0 in the low half of .x): an
+// accumulator quad (registers 4q..4q+3 = 4 consecutive rows, column = lane)
+// becomes one 8-byte row-contiguous store per lane.  Two DPP exchanges.
+DEV v2u32 quad_transpose4(uint32_t P0, uint32_t P1, int L) {
+  const bool up = L & 2, odd = L & 1;
+  const uint32_t Y = __builtin_amdgcn_update_dpp(0u, up ? P0 : P1, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+  const uint32_t Q0 = up ? Y : P0, Q1 = up ? P1 : Y;  // rows 2(L>>1)+{0,1} of columns L&1, (L&1)+2
+  const uint32_t S = odd ? ((Q0 & 0xFFFFu) | (Q1 << 16)) : ((Q0 >> 16) | (Q1 & 0xFFFF0000u));
+  const uint32_t R = __builtin_amdgcn_update_dpp(0u, S, 0xB1, 0xF, 0xF, false);            // lane ^ 1
+  v2u32 w;
+  if (!odd) {
+    w.x = (Q0 & 0xFFFFu) | (R << 16);
+    w.y = (Q1 & 0xFFFFu) | (R & 0xFFFF0000u);
+  } else {
+    w.x = (R & 0xFFFFu) | (Q0 & 0xFFFF0000u);
+    w.y = (R >> 16) | (Q1 & 0xFFFF0000u);
+  }
+  return w;
+}
+
 // ---- dropout: Philox4x32-10 (Salmon et al., SC'11; Random123 constants)
 // keyed by the 64-bit step seed.  A counter names a group of 4 consecutive
 // rows at one column, and the 4 output words are the 4 rows' draws, which
@@ -240,6 +263,10 @@ DEV uint4 edge_words(const Drop& d, int c, int i, int j, int t) {
 DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x * d.scale : 0.0f; }
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// cache-policy operand of the raw buffer builtins: nontemporal (gfx950 NT bit),
+// for write-once streams that are read back only by a later kernel (measured:
+// -5 % on k_prop_bwd's dM^T stream, and less L2 pollution for the next kernel)
+constexpr int kNT = 2;
 DEV rsrc_t mkrsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
@@ -284,6 +311,8 @@ DEV void st_col4(ActT<PREC>* dst, float a, float b, float c, float d) {
 // mode is bf16), i.e. the split mode runs k_wgrad with single f16 operands.
 template <int PREC>
 DEV void st_col4w(u16* dst, float a, float b, float c, float d) {
+  // (a nontemporal store here measured 10 % slower end to end: these 8-byte
+  // stores are 2N bytes apart across lanes and rely on L2 write combining)
   *(uint2*)dst = make_uint2(pk<Prec<PREC>::f16>(a, b), pk<Prec<PREC>::f16>(c, d));
 }
 template <int PREC> struct WgradPrec { static constexpr int value = Prec<PREC>::split ? PREC_F16 : PREC; };

@@ -48,11 +48,12 @@ __global__ void k_copy_f32(const float* __restrict__ s, float* __restrict__ d, l
 //       chunks 1 and 2 swapped) = the k order of an accumulator-as-B operand
 //       (k_prop_fwd's AGG);
 //   AbT [V][V] bf16 = A^T, natural order (B operand of k_prop_bwd);
-//   deg [V] fp32 = row sums (in-degree per channel, for dL/dbeta).
+//   deg [V] 16-bit limbs = row sums (in-degree per channel, <= 128: exact),
+//       the B operand of k_prop_bwd's dL/dbeta product.
 template <int V, bool F16>
 __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, int vin,
                                                   u16* __restrict__ Ab, u16* __restrict__ AbT,
-                                                  float* __restrict__ deg) {
+                                                  u16* __restrict__ deg) {
   __shared__ u16 t[V][V + 2];
   const long tile = blockIdx.x;  // g*C + c
   const float* src = A + tile * (long)vin * vin;
@@ -73,7 +74,7 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
   if (threadIdx.x < V) {
     float s = 0.f;
     for (int j = 0; j < V; ++j) s += from_limb<F16>(t[threadIdx.x][j]);
-    deg[tile * V + threadIdx.x] = s;
+    deg[tile * V + threadIdx.x] = to_limb<F16>(s);
   }
 }
 
@@ -170,5 +171,17 @@ __global__ void k_dropout_mask(int kind, int C, int H, int b, int vin, int t, Dr
       w = u4_get(state_words(dr, g, i, k, t), i & 3);
     }
     m[q] = (dr.thr == 0 || w < dr.thr) ? 1 : 0;
+  }
+}
+
+// out[e] += sum_g part[g][e]  (dL/dbeta from k_prop_bwd's per-(timestep, graph)
+// partials): blockIdx.y takes a slice of the rows, one atomic per slice
+__global__ void k_sum_graphs(const float* __restrict__ part, float* __restrict__ out, int rows, long E) {
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int g0 = blockIdx.y * per, g1 = min(rows, g0 + per);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int g = g0; g < g1; ++g) s += part[(long)g * E + e];
+    if (g1 > g0) atomicAdd(out + e, s);
   }
 }

@@ -71,8 +71,10 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     };
     // measured (config 3): the ring pays in the 3-product split mode, the
     // fully unrolled direct loop in the single-product modes
+#ifndef EXP_NO_MT
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
+#endif
     __syncthreads();  // S1: A_c visible
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
@@ -83,8 +85,10 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
       for (int it = 0; it < VT; ++it) {
         const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
         const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
+#ifndef EXP_NO_AGG
         mma_xa<PREC>(accx[it], a0, mh0, ml0);
         mma_xa<PREC>(accx[it], a1, mh1, ml1);
+#endif
       }
     }
     __syncthreads();  // S2: A_c reads done
@@ -129,13 +133,14 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 //                                                registers for all channels)
 //   dM_c -> LDS [j][n] image(s); dM_c^T -> HBM (weight-gradient operand)
 //   dh[j][k]   += sum_n dM_c[j][n] W_c[k][n]     (K = H)
-//   dbeta_c[n] += sum_i deg_c[i] dX[i][n]        (= sum_j dM_c[j][n])
+//   dbeta_c[n] += sum_i deg_c[i] dX[i][n]        (= sum_j dM_c[j][n]; per-graph
+//                                                partials dbp [b][C][H])
 // ===========================================================================
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
-k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const float* __restrict__ deg,
+k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
            const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
-           u16* __restrict__ dMT, float* __restrict__ dbeta, int C, long N, Drop dr, int tm) {
+           u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
@@ -180,68 +185,85 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     for (int r = 0; r < 16; ++r) adh[jt][r] = bld(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
   __syncthreads();
 
-  // dM^T store target: element (jt, r) of this lane sits at
-  //   dMT + (c*H + ns*32 + 4hh + acc_row0(r)) * N + rowg + jt*32 + l32
   for (int c = 0; c < C; ++c) {
-    if (dbeta) {
-      const float* dg = deg + ((long)g * C + c) * V;
-      float s = 0.f;
-#pragma unroll
-      for (int ss = 0; ss < KV; ++ss) {
-        const float4 d0 = *(const float4*)(dg + 16 * ss + 8 * hh);
-        const float4 d1 = *(const float4*)(dg + 16 * ss + 8 * hh + 4);
-        float x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = limb_elem<F16>(dxh[ss], j) + (SPLIT ? limb_elem<F16>(dxl[ss], j) : 0.f);
-        s += d0.x * x[0] + d0.y * x[1] + d0.z * x[2] + d0.w * x[3] + d1.x * x[4] + d1.y * x[5] + d1.z * x[6] +
-             d1.w * x[7];
-      }
-      s += __shfl_xor(s, 32);
-      if (hh == 0) atomicAdd(dbeta + c * H + n, s);
-    }
     // ---- phase a: dM_c^T tile (rows n of this wave), one 32-column j tile at a time
+    v2u32 dq[VT][4];  // f16(dM^T) quad-transposed for the deferred HBM store
 #pragma unroll
     for (int jt = 0; jt < VT; ++jt) {
       f32x16 am = splat(0.f);
+#ifndef EXP_NO_PHASE_A
 #pragma unroll
       for (int s = 0; s < KV; ++s) {
         const frag b = lds_frag(abuf, SA::off(jt * 32 + l32, 2 * s + hh));
         mma_xb<PREC>(am, dxh[s], dxl[s], b);
       }
+#endif
       const int j = jt * 32 + l32;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = ns * 32 + 8 * q + 4 * hh;
-        *(uint2*)(m_hi + SH::eoff(j, n0)) =
-            make_uint2(pk<F16>(am[4 * q], am[4 * q + 1]), pk<F16>(am[4 * q + 2], am[4 * q + 3]));
+        const uint32_t p0 = pk<F16>(am[4 * q], am[4 * q + 1]), p1 = pk<F16>(am[4 * q + 2], am[4 * q + 3]);
+        *(uint2*)(m_hi + SH::eoff(j, n0)) = make_uint2(p0, p1);
         if constexpr (SPLIT)
           *(uint2*)(m_lo + SH::eoff(j, n0)) =
               make_uint2(pk_lo<true>(am[4 * q], am[4 * q + 1]), pk_lo<true>(am[4 * q + 2], am[4 * q + 3]));
+        dq[jt][q] = quad_transpose4(p0, p1, l32 & 3);
       }
-      if (dMT) {
-        const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
-        const int vm = (int)((((long)ns * 32 + 4 * hh) * N + rowg + j) * 2);
+    }
+#ifndef EXP_NO_DBETA
+    if (dbp) {
+#else
+    if (false) {
+#endif
+      // dbeta_c[n] = sum_i dX[i][n] deg_c[i] as one more MFMA product: B[i][*] =
+      // deg_c[i] (exact integers), every output column holds the sum.  Per-graph
+      // partials [b][C][H] (no atomics); reduced over graphs after the last step.
+      const uint4* dg = (const uint4*)(deg + ((long)g * C + c) * V);  // wave-uniform: scalar loads
+      f32x16 db = splat(0.f);
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b16(to_limb<F16>(am[r]), rdm, vm, (int)(acc_row0(r) * N * 2), 0);
+      for (int ss = 0; ss < KV; ++ss) {
+        const uint4 d0 = dg[2 * ss], d1 = dg[2 * ss + 1];
+        mma_xb<PREC>(db, dxh[ss], dxl[ss], hh ? d1 : d0);
       }
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v = (r == (l32 & 15)) ? db[r] : v;
+      if (l32 < 16) dbp[((long)g * C + c) * H + ns * 32 + acc_row(l32, hh)] = v;
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
     // A_{c+1} lands in LDS by DMA while phase b runs (drained by S2)
     if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    b_direct<KS, 2>(
-        [&](int ks) { return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}}; },
-        [&](int ks, const F2& w) {
+    const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
+    const int vm = (int)((((long)ns * 32 + 4 * hh + (l32 & 3)) * N + rowg + 4 * (l32 >> 2)) * 2);
+#ifndef EXP_NO_PHASE_B
+#pragma unroll 2
+    for (int ks = 0; ks < KS; ++ks) {
+      const frag bh = frag_ld(wt, ns, ks, KS, lane);
+      const frag bl = SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : bh;
 #pragma unroll
-          for (int jt = 0; jt < VT; ++jt) {
-            const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
-            const frag ah = lds_frag(m_hi, off);
-            const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-            mma<PREC>(adh[jt], ah, al, w.a, w.b);
-          }
-        });
+      for (int jt = 0; jt < VT; ++jt) {
+        const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
+        const frag ah = lds_frag(m_hi, off);
+        const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
+        mma<PREC>(adh[jt], ah, al, bh, bl);
+      }
+    }
+#endif
+    // dM_c^T -> HBM [c][n][N] (weight-gradient operand).  Issued after the last
+    // weight-fragment wait of the channel: vmcnt is in order, so a store ahead of
+    // a load would make that load's wait cover the store too.  The stores then
+    // drain during the next channel's phase a, which has no vector-memory loads.
+#ifndef EXP_NO_DMT
+    if (dMT) {
+#pragma unroll
+      for (int jt = 0; jt < VT; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          __builtin_amdgcn_raw_buffer_store_b64(dq[jt][q], rdm, vm + jt * 64, 8 * q * N * 2, kNT);
+    }
+#endif
     __syncthreads();  // S2: dM image reads done, A_{c+1} staged
   }
   const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
