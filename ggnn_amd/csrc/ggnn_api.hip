@@ -319,20 +319,28 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   const PackL PL = pack_layout(c);
   const AdjL AL = adj_layout(c);
   const long N = c.N, H = c.H;
+  // unpadded batch (v a multiple of 32): the caller's h0 / hT are the engine's
+  // row layout, so inference reads h0 in place and the last step writes hT in
+  // place (training copies h0: the backward needs it after the caller's buffer
+  // may have changed)
+  const bool dense = c.vin == c.V;
   float* hf0 = tr ? P<float>(ws, L.hfT) : P<float>(ws, L.hf[0]);
-  {
-    Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H, hf0,
-                       SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N, (int)Prec<PREC>::f16, kNoDrop, 0);
-  }
   if (tr) {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL((k_transpose<float, u16, Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, hf0,
-                       P<u16>(ws, L.hT), N, c.H);
+    hipLaunchKernelGGL((k_stage_h0<Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, h0, c.vin, c.V,
+                       hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), P<u16>(ws, L.hT), N, c.H);
+  } else if (!dense || !SPLIT) {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H,
+                       dense ? (float*)nullptr : hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N,
+                       (int)Prec<PREC>::f16, kNoDrop, 0);
   }
   for (int t = 0; t < c.T; ++t) {
-    const float* hf_in = tr ? P<float>(ws, L.hfT + L.nh4 * t) : P<float>(ws, L.hf[t & 1]);
-    float* hf_out = tr ? P<float>(ws, L.hfT + L.nh4 * (t + 1)) : P<float>(ws, L.hf[(t + 1) & 1]);
+    const float* hf_in = tr ? P<float>(ws, L.hfT + L.nh4 * t)
+                            : (t == 0 && dense) ? h0 : P<float>(ws, L.hf[t & 1]);
+    float* hf_out = (t + 1 == c.T && dense) ? hT
+                    : tr                   ? P<float>(ws, L.hfT + L.nh4 * (t + 1))
+                                           : P<float>(ws, L.hf[(t + 1) & 1]);
     const u16* hb_in = SPLIT ? nullptr : P<u16>(ws, L.hb[t & 1]);
     u16* hb_out = SPLIT ? nullptr : P<u16>(ws, L.hb[(t + 1) & 1]);
     const void* hs = SPLIT ? (const void*)hf_in : (const void*)hb_in;
@@ -347,7 +355,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
                  co, rhT, s);
   }
   const float* hfin = tr ? P<float>(ws, L.hfT + L.nh4 * c.T) : P<float>(ws, L.hf[c.T & 1]);
-  {
+  if (!dense) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, hfin, c.vin, c.V, c.H, hT,
                        (long)c.b);
@@ -375,22 +383,29 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   if (use_bias) HIPCHK(hipMemsetAsync(dbeta, 0, (size_t)c.C * H * 4, s));
   float* dA = P<float>(ws, L.dA);
   float* dB = P<float>(ws, L.dB);
-  {
+  // unpadded batch without state dropout: dL/dh_T is read in place and the
+  // last step writes dL/dh0 in place
+  const bool dense = c.vin == c.V;
+  const bool in_place = dense && !c.sd;
+  if (!in_place) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
                        c.sdrop, c.T - 1);
   }
   for (int t = c.T - 1; t >= 0; --t) {
-    DISPATCH_HRT(c, launch_gru_bwd, PREC, c, dA, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
+    const float* delta = (t == c.T - 1 && in_place) ? dhT : dA;
+    float* dh_out = (t == 0 && dense) ? dh0 : dA;
+    DISPATCH_HRT(c, launch_gru_bwd, PREC, c, delta, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg, s);
     DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg), PL, pack,
-                dB, dA, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr, s);
+                dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr, s);
   }
   {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
-                       (long)c.b);
+    if (!dense)
+      hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
+                         (long)c.b);
     if (use_bias)
       hipLaunchKernelGGL(k_sum_graphs, dim3(grid1d((long)c.C * H, 64), 64), dim3(64), 0, s, P<const float>(ws, L.dbp),
                          dbeta, c.T * c.b, (long)c.C * H);

@@ -56,6 +56,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     return F4{frag_ld(Wgp, ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, ns, k, KSG, lane) : frag{},
               frag_ld(Wgp, NS + ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, k, KSG, lane) : frag{}};
   };
+#ifndef EXP_GF_NO_PASSA
   b_pipeline<KSG, 2>(ldg, [&](int k, const F4& w) {
     const char* ih = (k < KS) ? x_hi : h_hi;
     const char* il = (k < KS) ? x_lo : h_lo;
@@ -68,6 +69,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(au[rt], ah, al, w.c, w.d);
     }
   });
+#endif
   const rsrc_t rh_in = mkrsrc(hf + row0 * H, R * H * 4);
   const int vo = (4 * hh * H + n) * 4;
 #pragma unroll
@@ -78,7 +80,11 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       au[rt][r] = sigm(au[rt][r]);
     }
   __syncthreads();  // every wave is done reading the h image
-  // ---- r*h -> h image(s) and (training) r*h^T
+  // ---- r*h -> h image(s).  The r and (r*h)^T stores wait for the epilogue:
+  // vmcnt is in order, so a store issued here would make every weight-fragment
+  // wait of pass B cover it.
+  // (At RT = 4 keeping r live through pass B spills: store early there.)
+  constexpr bool DEFER = RT <= 2;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     float rh[16];
@@ -87,16 +93,18 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       rh[r] = ar[rt][r] * bld(rh_in, vo, (rt * 32 + acc_row0(r)) * H * 4);
       img_put<PREC, HCH>(h_hi, h_lo, rt * 32 + acc_row(r, hh), n, rh[r]);
     }
-    if (rhT_out) {
+    if constexpr (!DEFER) {
+      if (rhT_out) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
-                       rh[4 * q + 2], rh[4 * q + 3]);
-    }
-    if (r_out) {
-      const rsrc_t ro = mkrsrc(r_out + row0 * H, R * H * 4);
+        for (int q = 0; q < 4; ++q)
+          st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
+                         rh[4 * q + 2], rh[4 * q + 3]);
+      }
+      if (r_out) {
+        const rsrc_t ro = mkrsrc(r_out + row0 * H, R * H * 4);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bst(ro, ar[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
+        for (int r = 0; r < 16; ++r) bst(ro, ar[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
+      }
     }
   }
   __syncthreads();
@@ -111,6 +119,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     return F4{frag_ld(Wcp, ns, ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : frag{},
               frag_ld(Wcp, ns, KS + ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : frag{}};
   };
+#ifndef EXP_GF_NO_PASSB
   b_pipeline<KS, 2>(ldc, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -121,6 +130,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(ac[rt], qh, ql, w.c, w.d);
     }
   });
+#endif
   // ---- blend + outputs
   const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
   uint4 dw = make_uint4(0, 0, 0, 0);
@@ -132,7 +142,8 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       const int so = (rt * 32 + acc_row0(r)) * H * 4;
       const float cc = tanh_f(ac[rt][r]);
       const float u = au[rt][r];
-      float hn = u * bld(rh_in, vo, so) + (1.0f - u) * cc;
+      const float hprev = bld(rh_in, vo, so);
+      float hn = u * hprev + (1.0f - u) * cc;
       if (dr.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
         if ((r & 3) == 0) {
           const long grow = row0 + rt * 32 + acc_row0(r) + 4 * hh;
@@ -144,9 +155,17 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       if (u_out) {
         bst(mkrsrc(u_out + row0 * H, R * H * 4), u, vo, so);
         bst(mkrsrc(c_out + row0 * H, R * H * 4), cc, vo, so);
+        if constexpr (DEFER) bst(mkrsrc(r_out + row0 * H, R * H * 4), ar[rt][r], vo, so);
       }
+      if (DEFER && rhT_out) au[rt][r] = ar[rt][r] * hprev;  // r*h (u is dead from here)
       ac[rt][r] = hn;
       if constexpr (!SPLIT) *(u16*)(h_hi + SH::eoff(rt * 32 + acc_row(r, hh), n)) = to_limb<F16>(hn);
+    }
+    if (DEFER && rhT_out) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, au[rt][4 * q], au[rt][4 * q + 1],
+                       au[rt][4 * q + 2], au[rt][4 * q + 3]);
     }
     if (hT_out) {
 #pragma unroll
@@ -231,6 +250,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
               frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
   };
+#ifndef EXP_GB_NO_P1
   b_pipeline<KS, 2>(ld1, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -240,6 +260,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
   });
+#endif
   __syncthreads();  // dzc reads done
 
   // ---- phase 2: dh (into a2), dzg
@@ -280,6 +301,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
               frag_ld(WgTp, NS + ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
   };
+#ifndef EXP_GB_NO_P2
   b_pipeline<2 * KS, 2>(ld2, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -289,6 +311,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
   });
+#endif
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {

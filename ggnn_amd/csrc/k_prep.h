@@ -185,3 +185,32 @@ __global__ void k_sum_graphs(const float* __restrict__ part, float* __restrict__
     if (g1 > g0) atomicAdd(out + e, s);
   }
 }
+
+// Training-forward staging of h0 in one pass: h0 [b][vin][H] fp32 -> hf [N][H]
+// fp32 (pad rows zero), optional hb (16-bit limbs), and hT [H][N] (16-bit
+// limbs, the weight-gradient operand of timestep 0).  64x64 tiles via LDS.
+template <bool F16>
+__global__ void __launch_bounds__(256) k_stage_h0(const float* __restrict__ h0, int vin, int V, float* __restrict__ hf,
+                                                  u16* __restrict__ hb, u16* __restrict__ hT, long N, int H) {
+  __shared__ float t[64][65];
+  const long r0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  for (int q = threadIdx.x; q < 64 * 16; q += 256) {
+    const int i = q / 16, j4 = (q % 16) * 4;
+    const long row = r0 + i;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < N) {
+      const long g = row / V;
+      const int iv = (int)(row % V);
+      if (iv < vin) x = *(const float4*)(h0 + (g * vin + iv) * H + c0 + j4);
+      *(float4*)(hf + row * H + c0 + j4) = x;
+      if (hb) *(uint2*)(hb + row * H + c0 + j4) = make_uint2(pk<F16>(x.x, x.y), pk<F16>(x.z, x.w));
+    }
+    t[i][j4] = x.x; t[i][j4 + 1] = x.y; t[i][j4 + 2] = x.z; t[i][j4 + 3] = x.w;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
+    const int j = q / 64, i = q % 64;
+    if (r0 + i < N) hT[(long)(c0 + j) * N + r0 + i] = to_limb<F16>(t[i][j]);
+  }
+}
