@@ -277,8 +277,9 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
 #define DISPATCH_RT(c, FN, H, PREC, ...)                                             \
   do {                                                                               \
     constexpr bool sp_ = Prec<PREC>::split;                                          \
-    const int rt_ = gru_rt(c, sp_ ? 2 : kMaxRT<FN##_tag, H>::value);                 \
-    if (!sp_ && rt_ == 4) FN<H, sp_ ? 2 : 4, PREC>(__VA_ARGS__);                     \
+    constexpr int mx_ = sp_ ? 2 : kMaxRT<FN##_tag, H>::value;                        \
+    const int rt_ = gru_rt(c, mx_);                                                  \
+    if (mx_ >= 4 && rt_ == 4) FN<H, mx_ >= 4 ? 4 : 2, PREC>(__VA_ARGS__);            \
     else if (rt_ == 2) FN<H, 2, PREC>(__VA_ARGS__);                                  \
     else FN<H, 1, PREC>(__VA_ARGS__);                                                \
   } while (0)

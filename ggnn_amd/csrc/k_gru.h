@@ -218,28 +218,36 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   const int vo = (4 * hh * H + n) * 4;
   const long tcol = (long)n * N + row0 + 4 * hh;
 
-  // ---- phase 1: dzc
-  float csum = 0.f;
+  // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
+  // delta, u, c, h; delta*u stays in registers for phase 2's dh
+  float csum = 0.f, usum = 0.f;
+  float du[RT][16];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float dz[4];
+      float dz[4], zu[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld(pd, vo, so), u = bld(pu, vo, so), c = bld(pc, vo, so);
+        const float d = bld(pd, vo, so), u = bld(pu, vo, so), c = bld(pc, vo, so), h = bld(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
+        zu[i] = d * (h - c) * u * (1.0f - u);
+        du[rt][4 * q + i] = d * u;
         csum += dz[i];
+        usum += zu[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
+        img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, H + n, zu[i]);  // K >= H: not read by product 1
       }
       st_col4w<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
+      st_col4w<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
       __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
     }
   }
   csum += __shfl_xor(csum, 32);
-  if (hh == 0) atomicAdd(dbc + n, csum);
+  usum += __shfl_xor(usum, 32);
+  if (hh == 0) { atomicAdd(dbc + n, csum); atomicAdd(dbg + H + n, usum); }
   __syncthreads();
 
   // ---- product 1: [dX1 | d(rh)] = dzc @ Wc^T
@@ -263,37 +271,31 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #endif
   __syncthreads();  // dzc reads done
 
-  // ---- phase 2: dh (into a2), dzg
-  float rsum = 0.f, usum = 0.f;
+  // ---- phase 2: dh (into a2), the r half of dzg
+  float rsum = 0.f;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float zr[4], zu[4];
+      float zr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * q + i;
         const int ro = rt * 32 + acc_row0(r);
         const int so = ro * H * 4;
-        const float d = bld(pd, vo, so), h = bld(ph, vo, so), rr = bld(pr, vo, so), u = bld(pu, vo, so),
-                    c = bld(pc, vo, so);
+        const float h = bld(ph, vo, so), rr = bld(pr, vo, so);
         const float drh = a2[rt][r];
-        a2[rt][r] = d * u + drh * rr;
+        a2[rt][r] = du[rt][r] + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);
-        zu[i] = d * (h - c) * u * (1.0f - u);
         rsum += zr[i];
-        usum += zu[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
-        img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, H + n, zu[i]);
       }
       st_col4w<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
-      st_col4w<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
   rsum += __shfl_xor(rsum, 32);
-  usum += __shfl_xor(usum, 32);
-  if (hh == 0) { atomicAdd(dbg + n, rsum); atomicAdd(dbg + H + n, usum); }
+  if (hh == 0) atomicAdd(dbg + n, rsum);
   __syncthreads();
 
   // ---- product 2: [dX2 | dh2] = dzg @ Wg^T

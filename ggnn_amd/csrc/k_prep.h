@@ -54,22 +54,38 @@ template <int V, bool F16>
 __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, int vin,
                                                   u16* __restrict__ Ab, u16* __restrict__ AbT,
                                                   u16* __restrict__ deg) {
-  __shared__ u16 t[V][V + 2];
+  constexpr int P = V + 8;           // row pitch (u16): 16-B aligned rows, odd dword pitch / 4
+  __shared__ __attribute__((aligned(16))) u16 t[V][P];   // A[i][j]
+  __shared__ __attribute__((aligned(16))) u16 tt[V][P];  // A[j][i] (transposed)
   const long tile = blockIdx.x;  // g*C + c
   const float* src = A + tile * (long)vin * vin;
-  for (int q = threadIdx.x; q < V * V; q += 256) {
-    const int i = q / V, j = q % V;
-    t[i][j] = to_limb<F16>((i < vin && j < vin) ? src[i * vin + j] : 0.0f);
+  if (vin == V) {  // unpadded: 16-byte loads
+    for (int q = threadIdx.x; q < V * V / 4; q += 256) {
+      const int i = q / (V / 4), j = (q % (V / 4)) * 4;
+      const float4 x = *(const float4*)(src + i * V + j);
+      const u16 a0 = to_limb<F16>(x.x), a1 = to_limb<F16>(x.y), a2 = to_limb<F16>(x.z), a3 = to_limb<F16>(x.w);
+      *(uint2*)&t[i][j] = make_uint2(a0 | ((uint32_t)a1 << 16), a2 | ((uint32_t)a3 << 16));
+      tt[j][i] = a0; tt[j + 1][i] = a1; tt[j + 2][i] = a2; tt[j + 3][i] = a3;
+    }
+  } else {
+    for (int q = threadIdx.x; q < V * V; q += 256) {
+      const int i = q / V, j = q % V;
+      const u16 a = to_limb<F16>((i < vin && j < vin) ? src[i * vin + j] : 0.0f);
+      t[i][j] = a;
+      tt[j][i] = a;
+    }
   }
   __syncthreads();
   u16* ab = Ab + tile * V * V;
   u16* at = AbT + tile * V * V;
-  for (int q = threadIdx.x; q < V * V; q += 256) {
-    const int i = q / V, p = q % V;
-    const int grp = p & ~15, w = p & 15;
-    const int j = grp + ((w < 4) ? w : (w < 8) ? w + 4 : (w < 12) ? w - 4 : w);
-    ab[q] = t[i][j];
-    at[q] = t[p][i];
+  for (int q = threadIdx.x; q < V * V / 8; q += 256) {
+    const int i = q / (V / 8), p = (q % (V / 8)) * 8;  // 8 outputs [p, p+8) of row i
+    // Ab column order: inside every 16-column group the 8-byte chunks 1 and 2
+    // are swapped (p..p+7 = columns g+0..3, g+8..11 or g+4..7, g+12..15)
+    const int g16 = p & ~15, c0 = g16 + ((p & 8) ? 4 : 0);
+    const uint2 lo = *(const uint2*)&t[i][c0], hi = *(const uint2*)&t[i][c0 + 8];
+    *(uint4*)(ab + i * V + p) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    *(uint4*)(at + i * V + p) = *(const uint4*)&tt[i][p];
   }
   if (threadIdx.x < V) {
     float s = 0.f;
