@@ -177,21 +177,28 @@ DEV frag frag_ld(const u16* base, int strip, int ks, int nks, int lane) {
 // registers.
 struct F2 { frag a, b; };
 struct F4 { frag a, b, c, d; };
-template <int KS, int D, typename LD, typename BODY>
+// UNROLL: 0 = fully unrolled k loop (exact vmcnt counts everywhere), else the
+// outer loop is unrolled by that factor (smaller code and register live ranges;
+// the waitcnt pass is conservative at the loop head).
+template <int KS, int D, int UNROLL = 0, typename LD, typename BODY>
 DEV void b_pipeline(LD&& ld, BODY&& body) {
   static_assert(KS % D == 0, "k-steps must be a multiple of the pipeline depth");
   using FB = decltype(ld(0));
   FB ring[D];
 #pragma unroll
   for (int p = 0; p < D; ++p) ring[p] = ld(p);
-#pragma unroll 1
+#pragma unroll (UNROLL == 0 ? KS / D : UNROLL)
   for (int k0 = 0; k0 < KS; k0 += D) {
 #pragma unroll
     for (int p = 0; p < D; ++p) {
-      const int ks = k0 + p;
-      const FB cur = ring[p];
-      if (ks + D < KS) ring[p] = ld(ks + D);
-      body(ks, cur);
+      // consume slot p, then refill it: the refill is issued after the MFMAs
+      // that read the slot, so the slot keeps its registers (no copies, whose
+      // moves would force a vmcnt(0) on the younger loads)
+      // (unconditional, clamped: a branch here makes the waitcnt pass assume
+      // the worst case and emit vmcnt(0) at the loop head)
+      body(k0 + p, ring[p]);
+      ring[p] = ld(min(k0 + p + D, KS - 1));
+      __builtin_amdgcn_sched_barrier(0);  // keep the refill here (not sunk to the loop end)
     }
   }
 }

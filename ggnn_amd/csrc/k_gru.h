@@ -11,6 +11,10 @@
 #pragma once
 #include "ggnn_common.h"
 
+// weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
+// full unrolling, which spills at H = 256)
+constexpr int GF_UNROLL = 2, GB_UNROLL = 2;
+
 // ===========================================================================
 // k_gru_fwd
 //   pass A: [X | h] @ Wg            -> r, u      (K = 2H)
@@ -57,7 +61,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
               frag_ld(Wgp, NS + ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, k, KSG, lane) : frag{}};
   };
 #ifndef EXP_GF_NO_PASSA
-  b_pipeline<KSG, 2>(ldg, [&](int k, const F4& w) {
+  b_pipeline<KSG, 2, GF_UNROLL>(ldg, [&](int k, const F4& w) {
     const char* ih = (k < KS) ? x_hi : h_hi;
     const char* il = (k < KS) ? x_lo : h_lo;
     const int kk = (k < KS) ? k : k - KS;
@@ -120,7 +124,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
               frag_ld(Wcp, ns, KS + ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : frag{}};
   };
 #ifndef EXP_GF_NO_PASSB
-  b_pipeline<KS, 2>(ldc, [&](int ks, const F4& w) {
+  b_pipeline<KS, 2, GF_UNROLL>(ldc, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
@@ -259,7 +263,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
               frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
   };
 #ifndef EXP_GB_NO_P1
-  b_pipeline<KS, 2>(ld1, [&](int ks, const F4& w) {
+  b_pipeline<KS, 2, GB_UNROLL>(ld1, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
@@ -304,7 +308,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
               frag_ld(WgTp, NS + ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
   };
 #ifndef EXP_GB_NO_P2
-  b_pipeline<2 * KS, 2>(ld2, [&](int ks, const F4& w) {
+  b_pipeline<2 * KS, 2, GB_UNROLL>(ld2, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
