@@ -441,6 +441,9 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   memset(&a, 0, sizeof(a));
   int np = 0, tiles = 0;
   const long sa = (long)(L.nhw / 2);  // elements of one [H][N] weight-gradient operand array
+  // 256x256 tiles (k_wgrad256) at hidden = 256: every problem has M = 256
+  const bool big = H == 256 && N % 128 == 0;
+  const int TS = big ? 256 : 128;
   auto add = [&](size_t Poff, long stepP, size_t Qoff, long stepQ, float* out, int ldO, int M, int Nn, int nb = 1,
                  long sQb = 0, long sOb = 0) {
     WgProb& p = a.p[np++];
@@ -448,7 +451,7 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
     p.Q = P<u16>(ws, Qoff) + (long)t0 * stepQ;
     p.out = out;
     p.ldP = N; p.ldQ = N; p.stepP = stepP; p.stepQ = stepQ; p.sQb = sQb; p.sOb = sOb;
-    p.ldO = ldO; p.M = M; p.N = Nn; p.tiles_n = Nn / 128; p.tiles_b = (M / 128) * p.tiles_n;
+    p.ldO = ldO; p.M = M; p.N = Nn; p.tiles_n = Nn / TS; p.tiles_b = (M / TS) * p.tiles_n;
     p.sPb = 0; p.pdiv = 1; p.T = nt;
     p.tile_begin = tiles;
     tiles += nb * p.tiles_b;
@@ -472,6 +475,18 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   }
   constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
+  if (big) {
+    // one workgroup per CU (128 KiB LDS ring): the largest K chunk that still
+    // gives >= 7/8 of the CUs a tile-chunk
+    int KC = 8192;
+    while (KC > 128 && ((N % KC) != 0 || (long)tiles * (N / KC) < 224)) KC /= 2;
+    if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
+    a.KC = KC;
+    a.nchunks = (int)(N / KC);
+    Prof p(K_WGRAD, s);
+    hipLaunchKernelGGL((k_wgrad256<WP>), dim3(tiles * a.nchunks), dim3(512), 0, s, a);
+    return GGNN_OK;
+  }
   int KC = 4096;
   while (KC > 32 && (N % KC) != 0) KC /= 2;
   while (KC > 256 && (long)tiles * (N / KC) < 256) KC /= 2;

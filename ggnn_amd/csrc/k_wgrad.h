@@ -145,3 +145,119 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
         atomicAdd(outp + (long)m * pr.ldO + nn, acc[i][j][r]);
       }
 }
+
+// ===========================================================================
+// k_wgrad256: the same grouped NT problem set with 256x256 output tiles (all
+// problems have M = 256 and N a multiple of 256 at hidden = 256), so every
+// operand slice is read by one workgroup only (dW: P and Q once; dWg: P
+// twice).  8 waves as 2 (m) x 4 (n), 128x64 outputs each.  K slices of 32
+// rows arrive by LDS-DMA into a 4-deep ring: two slices stay in flight while
+// one is consumed (counted vmcnt + raw s_barrier; a __syncthreads would drain
+// the DMAs every step).  16-bit operands only (the split mode's weight-gradient
+// operands are single f16 limbs).
+// ===========================================================================
+// LDS-DMA of 16 B per lane in inline asm: invisible to hipcc's waitcnt pass,
+// which would otherwise wait vmcnt(0) before every ds_read of the ring (it
+// cannot tell the ring slots apart); completion is counted by hand below.
+DEV void glds16_asm(const void* gsrc, const char* lds_dst) {
+  unsigned keep;
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
+  constexpr bool F16 = Prec<PREC>::f16;
+  static_assert(!Prec<PREC>::split, "16-bit operands only");
+  constexpr int BK = 32, CH = BK / 8;        // 4 chunks of 16 B per image row
+  constexpr int TB = 256 * BK * 2;           // 16 KiB per operand image
+  constexpr int NBUF = 4;
+  constexpr int GPW = 256 * CH / 64 / 8;     // glds per wave per operand per slice (= 2)
+  // one __shared__ object per ring slot, each addressed with a compile-time
+  // slot index: the waitcnt pass can then tell a ds_read of slot u from the
+  // DMAs still landing in the other slots (with one array and a runtime slot
+  // it waits vmcnt(0) before every read)
+  __shared__ __attribute__((aligned(16))) char sp0[TB], sp1[TB], sp2[TB], sp3[TB];  // P images
+  __shared__ __attribute__((aligned(16))) char sq0[TB], sq1[TB], sq2[TB], sq3[TB];  // Q images
+  auto pslot = [&](int u) -> char* { return u == 0 ? sp0 : u == 1 ? sp1 : u == 2 ? sp2 : sp3; };
+  auto qslot = [&](int u) -> char* { return u == 0 ? sq0 : u == 1 ? sq1 : u == 2 ? sq2 : sq3; };
+  const int tile = blockIdx.x / args.nchunks, chunk = blockIdx.x % args.nchunks;
+  int pi = 0;
+  while (pi + 1 < args.nprob && args.p[pi + 1].tile_begin <= tile) ++pi;
+  const WgProb pr = args.p[pi];
+  const int lt0 = tile - pr.tile_begin;
+  const int bi = lt0 / pr.tiles_b, lt = lt0 % pr.tiles_b;
+  const int m0 = (lt / pr.tiles_n) * 256, n0 = (lt % pr.tiles_n) * 256;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int wm = wv >> 2, wn = wv & 3;
+  // image: row r = 64 B, chunk slot pc holds logical chunk pc ^ ((r >> 2) & 3)
+  auto soff = [](int row, int ch) { return row * BK * 2 + ((ch ^ ((row >> 2) & 3)) << 4); };
+
+  const int kits = args.KC / BK, nit = kits * pr.T;  // host guarantees nit % NBUF == 0
+  const long kbase = (long)chunk * args.KC;
+  const u16* Pb = (const u16*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
+  const u16* Qb = (const u16*)pr.Q + (long)bi * pr.sQb;
+  float* const outp = pr.out + (long)bi * pr.sOb;
+
+  auto stage = [&](int it, char* bp, char* bq) {
+    const int t = it / kits;
+    const long k0 = kbase + (long)(it % kits) * BK;
+    const u16* P = Pb + (long)t * pr.stepP + k0;
+    const u16* Q = Qb + (long)t * pr.stepQ + k0;
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      const int qb = (g * 8 + wv) * 64;  // first 16-B slot of this wave-instruction
+      const int q = qb + lane, row = q / CH, pc = q % CH, lc = pc ^ ((row >> 2) & 3);
+      glds16_asm(P + (long)(m0 + row) * pr.ldP + lc * 8, bp + qb * 16);
+      glds16_asm(Q + (long)(n0 + row) * pr.ldQ + lc * 8, bq + qb * 16);
+    }
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = splat(0.f);
+
+  // prologue: slices 0, 1, 2 in flight
+#pragma unroll
+  for (int u = 0; u < NBUF - 1; ++u) stage(u, pslot(u), qslot(u));
+  for (int it0 = 0; it0 < nit; it0 += NBUF) {
+#pragma unroll
+    for (int u = 0; u < NBUF; ++u) {
+      const int it = it0 + u;
+      // slice `it` landed (this wave's DMAs: the two younger slices may stay in flight)
+      if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory");
+      else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice `it` landed; slice it-1 fully read
+      if (it + NBUF - 1 < nit) stage(it + NBUF - 1, pslot((u + NBUF - 1) % NBUF), qslot((u + NBUF - 1) % NBUF));
+      const char* bp = pslot(u);
+      const char* bq = qslot(u);
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        frag a[4], bb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = lds_frag(bp, soff(wm * 128 + i * 32 + l32, 2 * s + hh));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bb[j] = lds_frag(bq, soff(wn * 64 + j * 32 + l32, 2 * s + hh));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma<F16>(a[i], bb[j], acc[i][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + i * 32 + acc_row(r, hh);
+        const int nn = n0 + wn * 64 + j * 32 + l32;
+        atomicAdd(outp + (long)m * pr.ldO + nn, acc[i][j][r]);
+      }
+}
