@@ -8,7 +8,7 @@ set -e
 TAG=${1:-r01}
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o bench -- \
-  python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_trace.log 2>&1
+  python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --dropout-keep 1 > gpurun_out/${TAG}_trace.log 2>&1
 bash tools/pmc_profile.sh gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc.log 2>&1
 cp gpurun_out/${TAG}_pmc/pmc_traffic.json profiles/pmc_traffic.json
 timeout -k 10 300 python3 bench.py > gpurun_out/${TAG}_bench.log 2>&1
