@@ -86,6 +86,44 @@ def cpu_baseline(seconds=10.0, sample_b=8):
                        % (sample_b, CFG["v"], CFG["h"], C, CFG["T"], n, el))
 
 
+def adjacency_feed_costs(eng, b, v, E, dev, reps=5):
+    """Side measurement (SURVEY §8f compact adjacency producer): staging one
+    batch of dependency-tree-shaped graphs (v-1 labelled edges each) from the
+    reference's dense [b, 2E, v, v] feed (host copy + ggnn_set_adjacency) vs
+    from edge lists (ggnn_set_adjacency_edges)."""
+    import torch
+    import ggnn_oracle as O
+    rng = np.random.default_rng(5)
+    graphs = []
+    for _ in range(b):
+        dst = np.arange(1, v)
+        src = np.array([rng.integers(0, i) for i in dst])       # a random tree: head before dependent
+        lab = rng.integers(1, E + 1, v - 1)
+        graphs.append(np.stack([src, lab, dst], 1).tolist())
+    A = np.stack([O.graph_to_adj_mat_bd(g, v, E) for g in graphs]).astype(np.float32)
+    A_host = torch.from_numpy(A)
+    A_dev = A_host.to(dev)
+    e_np = np.concatenate([np.asarray(g, np.int32) for g in graphs])
+    offs = np.arange(0, b * (v - 1) + 1, v - 1, dtype=np.int32)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    ms_dense_dev = timed(lambda: eng.set_adjacency(A_dev))
+    ms_dense_h2d = timed(lambda: eng.set_adjacency(A_host.to(dev)))
+    ms_edges_h2d = timed(lambda: eng.set_adjacency_edges(
+        (torch.from_numpy(e_np).to(dev), torch.from_numpy(offs).to(dev)), v, E))
+    return {"graphs": "random dependency trees, v-1 edges each", "dense_bytes": int(A.nbytes),
+            "edge_bytes": int(e_np.nbytes + offs.nbytes),
+            "dense_in_hbm_ms": ms_dense_dev, "dense_from_host_ms": ms_dense_h2d, "edges_from_host_ms": ms_edges_h2d}
+
+
 def load_traffic():
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -210,6 +248,8 @@ def main():
     breakdown = {k: {"ms_per_step": timer.total_ms[k] / args.steps, "launches_per_step": timer.launches[k] / args.steps}
                  for k in kinds}
 
+    feed_cmp = adjacency_feed_costs(eng, b, v, CFG["e"], dev) if rank == 0 else None
+
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]
         value = world * b / dt
@@ -236,6 +276,7 @@ def main():
             "achieved_step_tflops": world * b * fpg / dt / 1e12,
             "kernel_breakdown": breakdown,
             "ms_per_step_event_instrumented": dt_instr * 1e3,
+            "adjacency_feed": feed_cmp,
             "dropout_on": {"edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
                            "value": world * b / dt_drop, "ms_per_step": dt_drop * 1e3,
                            "note": "same step with the reference's training-feed dropout (:860-861); "

@@ -21,6 +21,7 @@ PRECISIONS = ("bf16", "fp16", "fp32")
 EXPORTED = (
     "ggnn_version", "ggnn_last_error", "ggnn_check_dims", "ggnn_workspace_bytes",
     "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
+    "ggnn_set_adjacency_edges",
     "ggnn_forward", "ggnn_backward", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end",
 )
@@ -76,6 +77,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_pack_weights.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P]
         lib.ggnn_set_adjacency.restype = _I
         lib.ggnn_set_adjacency.argtypes = [_DP, _P, _P, _P]
+        lib.ggnn_set_adjacency_edges.restype = _I
+        lib.ggnn_set_adjacency_edges.argtypes = [_DP, _P, _P, _P, ctypes.c_int64, _I, _P]
         lib.ggnn_forward.restype = _I
         lib.ggnn_forward.argtypes = [_DP, _P, _P, _P, _I, _P, _P, _P]
         lib.ggnn_backward.restype = _I

@@ -123,8 +123,13 @@ class BtbBatching:
             feats = self.vectorize_node_features(d["node_features"], v, d["graph"])
             xdim = len(feats[0])
             heads = [0] + [e[0] for e in d["graph"]]
+            # params['compact_adjacency']: keep only the edge list (the engine
+            # stages it on the device, ggnn_set_adjacency_edges) instead of the
+            # dense [2E, v, v] float64 matrix per graph
+            compact = bool(self.params.get("compact_adjacency", False))
             bucketed[bidx].append({
-                "adj_mat": graph_to_adj_mat_bd(d["graph"], v, self.num_edge_types),
+                "adj_mat": None if compact else graph_to_adj_mat_bd(d["graph"], v, self.num_edge_types),
+                "graph": d["graph"],
                 "init": feats + [np.zeros(xdim, dtype=np.int64) for _ in range(v - n)],
                 "labels": self.get_labels_padded(d, v, n),
                 "mask": self.get_mask(n, v),
@@ -152,7 +157,7 @@ class BtbBatching:
         return bucketed, bucket_sizes, bucket_at_step
 
     def make_batch(self, elements):
-        keys = ("adj_mat", "init", "node_mask", "node_mask_edges", "sentences_id", "words_pos",
+        keys = ("adj_mat", "graph", "init", "node_mask", "node_mask_edges", "sentences_id", "words_pos",
                 "words_loc", "words_index", "words_head", "words_head_pos", "edges_index", "target_pos")
         batch = {k: [] for k in keys}
         batch["labels"], batch["task_masks"] = [], []
@@ -212,7 +217,8 @@ class BtbBatching:
                 "target_mask": np.transpose(batch["task_masks"], axes=[1, 0]),
                 "num_graphs": b,
                 "num_vertices": v,
-                "adjacency_matrix": batch["adj_mat"],
+                "adjacency_matrix": None if batch["adj_mat"][0] is None else batch["adj_mat"],
+                "adjacency_edges": batch["graph"],
                 "node_mask": np.array(batch["node_mask"]),
                 "node_mask_edges": np.array(batch["node_mask_edges"]),
                 "graph_state_keep_prob": keep,

@@ -629,6 +629,39 @@ int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_s
   return GGNN_OK;
 }
 
+int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges, const int32_t* graph_offsets,
+                             int64_t num_edges, int num_edge_types, ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!adj || !graph_offsets || (num_edges > 0 && !edges)) return fail(GGNN_EINVAL, "set_adjacency_edges: NULL pointer");
+  if (num_edge_types < 1 || 2 * num_edge_types != c.C)
+    return fail(GGNN_EINVAL, "set_adjacency_edges: C must equal 2 * num_edge_types");
+  if (num_edges < 0) return fail(GGNN_EINVAL, "set_adjacency_edges: num_edges < 0");
+  hipStream_t s = (hipStream_t)stream;
+  const AdjL L = adj_layout(c);
+  const size_t tiles = (size_t)c.b * c.C;
+  Prof p(K_ADJ, s);
+  HIPCHK(hipMemsetAsync(P<u16>(adj, L.Ab), 0, tiles * c.V * c.V * 2, s));
+  HIPCHK(hipMemsetAsync(P<u16>(adj, L.AbT), 0, tiles * c.V * c.V * 2, s));
+  const int grid = grid1d(std::max<int64_t>(num_edges, 1));
+#define ADJ_EDGES(VV, F)                                                                                         \
+  do {                                                                                                           \
+    if (num_edges > 0)                                                                                           \
+      hipLaunchKernelGGL((k_adj_from_edges<VV, F>), dim3(grid), dim3(256), 0, s, edges, graph_offsets, c.b,      \
+                         c.vin, num_edge_types, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT));                           \
+    hipLaunchKernelGGL((k_adj_deg<VV, F>), dim3((unsigned)tiles), dim3(VV), 0, s, P<const u16>(adj, L.Ab),        \
+                       P<u16>(adj, L.deg));                                                                      \
+  } while (0)
+  const bool f16 = c.prec != PREC_BF16;
+  if (c.V == 32) { if (f16) ADJ_EDGES(32, true); else ADJ_EDGES(32, false); }
+  else if (c.V == 64) { if (f16) ADJ_EDGES(64, true); else ADJ_EDGES(64, false); }
+  else { if (f16) ADJ_EDGES(128, true); else ADJ_EDGES(128, false); }
+#undef ADJ_EDGES
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
 int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_stream_t stream) {
   Cfg c;
   int e = make_cfg(d, &c);

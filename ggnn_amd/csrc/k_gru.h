@@ -57,6 +57,9 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   }
   // ---- pass A over k in [0, 2H): x rows then h rows of Wg
   auto ldg = [&](int k) {
+#ifdef EXP_GF_W0
+    k = k & 1;
+#endif
     return F4{frag_ld(Wgp, ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, ns, k, KSG, lane) : frag{},
               frag_ld(Wgp, NS + ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, k, KSG, lane) : frag{}};
   };
@@ -120,6 +123,9 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     for (int rt = 0; rt < RT; ++rt) ac[rt] = splat(b0);
   }
   auto ldc = [&](int ks) {
+#ifdef EXP_GF_W0
+    ks = ks & 1;
+#endif
     return F4{frag_ld(Wcp, ns, ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : frag{},
               frag_ld(Wcp, ns, KS + ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : frag{}};
   };

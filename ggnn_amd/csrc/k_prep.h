@@ -230,3 +230,58 @@ __global__ void __launch_bounds__(256) k_stage_h0(const float* __restrict__ h0, 
     if (r0 + i < N) hT[(long)(c0 + j) * N + r0 + i] = to_limb<F16>(t[i][j]);
   }
 }
+
+// ---- compact adjacency producer (upload edge lists instead of the
+// dense [b][2E][v][v] float64 feed).  Restates graph_to_adj_mat_bd,
+// chem_tensorflow_dense.py:65-83, straight into the staged layouts: for every
+// edge (src, e, dest) of graph g
+//   A[e-1][dest][src] = A[e-1+E][src][dest] = A[E-1][dest][dest-1]
+//   = A[2E-1][dest-1][dest] = 1,
+// dest-1 = -1 wrapping to v-1 as numpy's negative index does.  Ab / AbT must be
+// zeroed first; a cell set twice stays 1.  Edges outside the graph (label not
+// in 1..E, node not in 0..v-1) are skipped (the Python layer rejects them).
+template <int V, bool F16>
+__global__ void k_adj_from_edges(const int* __restrict__ edges, const int* __restrict__ offs, int b, int vin, int E,
+                                 u16* __restrict__ Ab, u16* __restrict__ AbT) {
+  const u16 one = to_limb<F16>(1.0f);
+  const int C = 2 * E;
+  const long total = offs[b];
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    // graph of edge q: binary search in the offsets
+    int lo = 0, hi = b;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offs[mid] <= q) lo = mid; else hi = mid;
+    }
+    const int g = lo;
+    const int src = edges[3 * q], e = edges[3 * q + 1], dst = edges[3 * q + 2];
+    if (e < 1 || e > E || src < 0 || src >= vin || dst < 0 || dst >= vin) continue;
+    const int prev = dst >= 1 ? dst - 1 : vin - 1;
+    const int ch[4] = {e - 1, e - 1 + E, E - 1, 2 * E - 1};
+    const int ro[4] = {dst, src, dst, prev};
+    const int co[4] = {src, dst, prev, dst};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long tile = (long)g * C + ch[k];
+      const int i = ro[k], j = co[k];
+      const int w = j & 15, p = (j & ~15) + ((w < 4 || w >= 12) ? w : (w < 8) ? w + 4 : w - 4);
+      Ab[(tile * V + i) * V + p] = one;   // columns permuted as k_prep_adj writes them
+      AbT[(tile * V + j) * V + i] = one;
+    }
+  }
+}
+
+// deg[tile][i] = row sums of the staged adjacency (after k_adj_from_edges)
+template <int V, bool F16>
+__global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, u16* __restrict__ deg) {
+  const long tile = blockIdx.x;
+  const u16* row = Ab + (tile * V + threadIdx.x) * V;
+  float s = 0.f;
+  for (int j = 0; j < V; j += 8) {
+    const uint4 x = *(const uint4*)(row + j);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += from_limb<F16>((u16)(w[k] & 0xFFFF)) + from_limb<F16>((u16)(w[k] >> 16));
+  }
+  deg[tile * V + threadIdx.x] = to_limb<F16>(s);
+}

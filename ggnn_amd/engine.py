@@ -138,6 +138,47 @@ class PropagationEngine:
         self._batch = (int(b), int(v))
         self._trained = None
 
+    def set_adjacency_edges(self, graphs, v: int, num_edge_types: int) -> None:
+        """Stage a batch from the reference's edge lists (each graph a list of
+        (src, label, dest) triples, chem_tensorflow_dense.py:65-83) without
+        building the dense [b, 2E, v, v] feed: only the edge rows (12 B each)
+        cross PCIe.  ``graphs`` is a list of per-graph edge lists, or a tuple
+        (edges int32 [n, 3], graph_offsets int32 [b + 1]) already on the
+        device.  Raises IndexError for edges the reference would index out of
+        range."""
+        import numpy as np
+        E = int(num_edge_types)
+        if 2 * E != self.C:
+            raise ValueError("num_edge_types=%d does not match C=%d channels" % (E, self.C))
+        if isinstance(graphs, tuple):
+            edges, offs = graphs
+            b = int(offs.numel()) - 1
+            n = int(edges.shape[0])
+        else:
+            b = len(graphs)
+            sizes = [len(g) for g in graphs]
+            offs_np = np.zeros(b + 1, np.int32)
+            offs_np[1:] = np.cumsum(sizes)
+            n = int(offs_np[-1])
+            e_np = (np.concatenate([np.asarray(g, np.int32).reshape(-1, 3) for g in graphs if len(g)])
+                    if n else np.zeros((0, 3), np.int32))
+            if n:
+                src, lab, dst = e_np[:, 0], e_np[:, 1], e_np[:, 2]
+                if lab.min() < 1 or lab.max() > E:
+                    raise IndexError("edge label outside 1..%d" % E)
+                if min(src.min(), dst.min()) < 0 or max(src.max(), dst.max()) >= v:
+                    raise IndexError("edge node index outside 0..%d" % (v - 1))
+            edges = torch.from_numpy(np.ascontiguousarray(e_np)).to(self.device)
+            offs = torch.from_numpy(offs_np).to(self.device)
+        d = self.dims(b, v, 1)
+        nbytes = _lib.adjacency_bytes(d)
+        if self._adj is None or self._adj.numel() < nbytes:
+            self._adj = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        _lib.check(self._lib.ggnn_set_adjacency_edges(ctypes.byref(d), _ptr(self._adj), _ptr(edges), _ptr(offs),
+                                                      n, E, _stream()), "ggnn_set_adjacency_edges")
+        self._batch = (int(b), int(v))
+        self._trained = None
+
     @property
     def batch_shape(self):
         return self._batch

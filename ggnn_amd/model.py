@@ -106,6 +106,7 @@ class DenseGGNNChemModel(BtbBatching):
             "task_ids": [0], "random_seed": 0, "output_size": 150,
             "graph_state_dropout_keep_prob": 0.9, "task_sample_ratios": {}, "use_edge_bias": True,
             "edge_weight_dropout_keep_prob": 1,
+            "compact_adjacency": False,   # not in the reference: edge-list feed (ggnn_set_adjacency_edges)
         }
 
     @property
@@ -142,11 +143,18 @@ class DenseGGNNChemModel(BtbBatching):
     def feed(self, feed_dict: dict) -> None:
         """Stage one minibatch (a dict from ``make_minibatch_iterator`` or any
         dict with ``adjacency_matrix``, ``num_vertices``, ``num_graphs``)."""
-        adj = feed_dict["adjacency_matrix"]
+        adj = feed_dict.get("adjacency_matrix")
+        self.placeholders = dict(feed_dict)
+        if adj is None:
+            # compact feed: edge lists only (params['compact_adjacency'])
+            if feed_dict.get("adjacency_edges") is None:
+                raise ValueError("feed needs adjacency_matrix or adjacency_edges")
+            self.placeholders["adjacency_matrix"] = None
+            self._fed = False
+            return
         if not isinstance(adj, torch.Tensor):
             adj = torch.from_numpy(np.ascontiguousarray(np.asarray(adj, dtype=np.float32)))
         adj = adj.to(device=self.device, dtype=torch.float32).contiguous()
-        self.placeholders = dict(feed_dict)
         self.placeholders["adjacency_matrix"] = adj
         b, C, v, _ = adj.shape
         if C != self.num_channels:
@@ -169,7 +177,7 @@ class DenseGGNNChemModel(BtbBatching):
         """[b, v, h] -> [b, v, h] after T = num_timesteps (or fixed_ts) GGNN
         steps (chem_tensorflow_dense.py:312-340).  ``fixed_ts`` selects the
         ``*_fixed`` edge weights/biases, as compute_timestep_fast does (:396-412)."""
-        if "adjacency_matrix" not in self.placeholders:
+        if "adjacency_matrix" not in self.placeholders and "adjacency_edges" not in self.placeholders:
             raise RuntimeError("feed() a minibatch before compute_final_node_representations()")
         if self.args.get("--pr", "btb") not in ("btb",) or self.args.get("--old"):
             # the identity/--old variants compute the same contraction in another
@@ -186,7 +194,11 @@ class DenseGGNNChemModel(BtbBatching):
             h0 = torch.from_numpy(np.ascontiguousarray(np.asarray(h0, dtype=np.float32)))
         h0 = h0.to(device=self.device, dtype=torch.float32)
         eng = self._engine("main" if fixed_ts is None else "fixed")
-        eng.set_adjacency(self.placeholders["adjacency_matrix"])
+        if self.placeholders["adjacency_matrix"] is not None:
+            eng.set_adjacency(self.placeholders["adjacency_matrix"])
+        else:
+            eng.set_adjacency_edges(self.placeholders["adjacency_edges"], int(self.placeholders["num_vertices"]),
+                                    self.num_edge_types)
         gru = self.weights["node_gru"]
         # dropout as fed (chem_tensorflow_dense.py:860-861 training, :938-940 eval);
         # a fresh Philox seed per call = fresh masks per step, like TF's stateful RNG

@@ -121,6 +121,20 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack,
 int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* adjacency,
                        ggnn_stream_t stream);
 
+/* Stage one batch's adjacency from edge lists instead of the dense feed (the
+ * compact producer of SURVEY §8f): the same staged bytes as
+ * ggnn_set_adjacency(graph_to_adj_mat_bd(...)) (chem_tensorflow_dense.py:65-83,
+ * built per graph at :539) without the [b][2E][v][v] host array or its copy.
+ *   edges         device int32 [num_edges][3] = (src, label, dest) rows of the
+ *                 reference's 'graph' lists, graphs concatenated;
+ *   graph_offsets device int32 [b + 1]: graph g owns rows [off[g], off[g+1]);
+ *   num_edge_types E with d->C == 2E.
+ * Labels outside 1..E or nodes outside 0..v-1 are skipped (validate on the
+ * host: the reference raises IndexError for them). */
+int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges,
+                             const int32_t* graph_offsets, int64_t num_edges,
+                             int num_edge_types, ggnn_stream_t stream);
+
 /* T-step forward.  h0, hT: [b][v][h] fp32.  training != 0 keeps what the
  * backward needs inside ws (ws must have been sized with training != 0). */
 int ggnn_forward(const ggnn_dims* d, const void* pack, const void* adj, void* ws,

@@ -352,3 +352,90 @@ def test_drop_in_model_training_feed_applies_dropout():
     ref, _ = O.forward(np.asarray(fd["adjacency_matrix"], np.float64), h0.astype(np.float64), w64, 2,
                        keep_cache=False, dropout=m.last_dropout)
     assert np.abs(out.detach().cpu().numpy() - ref).max() <= FP32_TOL
+
+
+# ------------------------------------------------- compact adjacency producer
+def _random_graphs(rng, b, v, E, n_edges):
+    gs = []
+    for _ in range(b):
+        n = int(rng.integers(0, n_edges + 1))
+        src = rng.integers(0, v, n)
+        dst = rng.integers(0, v, n)          # includes dest = 0 (prev-word edge wraps to v-1, as numpy does)
+        lab = rng.integers(1, E + 1, n)
+        g = np.stack([src, lab, dst], 1).tolist()
+        if n > 1:
+            g.append(g[0])                   # a duplicate edge
+        gs.append(g)
+    return gs
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("b,v,E", [(3, 20, 2), (4, 64, 4), (2, 128, 4), (5, 50, 46)])
+def test_adjacency_from_edges_is_byte_identical(b, v, E, precision):
+    """ggnn_set_adjacency_edges stages exactly the bytes that ggnn_set_adjacency
+    stages from the reference's dense graph_to_adj_mat_bd feed."""
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    rng = np.random.default_rng(b * 100 + v + E)
+    graphs = _random_graphs(rng, b, v, E, 3 * v)
+    A = np.stack([O.graph_to_adj_mat_bd(g, v, E) for g in graphs]).astype(np.float32)
+    eng = PropagationEngine(128, 2 * E, precision=precision)
+    eng.set_adjacency(torch.from_numpy(A).to(eng.device))
+    dense = eng._adj.clone()
+    eng.set_adjacency_edges(graphs, v, E)
+    assert torch.equal(eng._adj[:dense.numel()], dense)
+
+
+def test_adjacency_from_edges_on_reference_dev_graphs():
+    """Real WSJ dev sentences (golden fixture, E = 46): the edge path feeds the
+    same forward as the reference's dense adjacency."""
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
+    data = json.loads(str(g["raw_json"]))
+    E, v = int(g["num_edge_types"]), 64
+    graphs = [d["graph"] for d in data[:12] if max(max(e[0], e[2]) for e in d["graph"]) < v]
+    A = np.stack([O.graph_to_adj_mat_bd(gr, v, E) for gr in graphs]).astype(np.float32)
+    eng = PropagationEngine(128, 2 * E, precision="fp32")
+    w = O.synthetic_weights(128, 2 * E, seed=4)
+    pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(eng.device) for k, x in w.items()})
+    h0 = torch.from_numpy(np.random.default_rng(0).uniform(-0.5, 0.5, (len(graphs), v, 128)).astype(np.float32))
+    h0 = h0.to(eng.device)
+    eng.set_adjacency(torch.from_numpy(A).to(eng.device))
+    a = eng.forward(h0, pack, 2).cpu().numpy()
+    eng.set_adjacency_edges(graphs, v, E)
+    b_ = eng.forward(h0, pack, 2).cpu().numpy()
+    assert np.array_equal(a, b_)
+
+
+def test_adjacency_from_edges_rejects_out_of_range():
+    _torch()
+    from ggnn_amd.engine import PropagationEngine
+    eng = PropagationEngine(128, 4)
+    with pytest.raises(IndexError):
+        eng.set_adjacency_edges([[[0, 3, 1]]], 8, 2)     # label 3 > E
+    with pytest.raises(IndexError):
+        eng.set_adjacency_edges([[[0, 1, 8]]], 8, 2)     # node 8 >= v
+
+
+def test_drop_in_model_compact_adjacency_feed():
+    """params['compact_adjacency']: batches carry edge lists only and the model
+    stages them on the device; outputs equal the dense-feed model's."""
+    torch = _torch()
+    from ggnn_amd.model import DenseGGNNChemModel
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
+    data = json.loads(str(g["raw_json"]))
+    outs = []
+    for compact in (False, True):
+        m = DenseGGNNChemModel(params={"hidden_size": 128, "num_timesteps": 2, "batch_size": 8,
+                                       "compact_adjacency": compact},
+                               num_edge_types=int(g["num_edge_types"]), output_size_edges=int(g["output_size_edges"]),
+                               pos_size=int(g["pos_size"]), bucket_max_nodes=int(g["bucket_max_nodes"]),
+                               precision="fp32", seed=3)
+        fd = next(iter(m.make_minibatch_iterator(m.process_raw_graphs(data[:16], False), False)))
+        assert (fd["adjacency_matrix"] is None) == compact
+        m.feed(fd)
+        h0 = np.random.default_rng(1).uniform(-0.5, 0.5, (fd["num_graphs"], fd["num_vertices"], 128))
+        outs.append(m.compute_final_node_representations(torch.from_numpy(h0.astype(np.float32)).to(m.device))
+                    .detach().cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
