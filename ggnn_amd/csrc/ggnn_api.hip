@@ -277,7 +277,7 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
 #define DISPATCH_RT(c, FN, H, PREC, ...)                                             \
   do {                                                                               \
     constexpr bool sp_ = Prec<PREC>::split;                                          \
-    constexpr int mx_ = sp_ ? 2 : kMaxRT<FN##_tag, H>::value;                        \
+    constexpr int mx_ = sp_ ? kSplitRT<FN##_tag>::value : kMaxRT<FN##_tag, H>::value; \
     const int rt_ = gru_rt(c, mx_);                                                  \
     if (mx_ >= 4 && rt_ == 4) FN<H, mx_ >= 4 ? 4 : 2, PREC>(__VA_ARGS__);            \
     else if (rt_ == 2) FN<H, 2, PREC>(__VA_ARGS__);                                  \
@@ -295,6 +295,13 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
 struct launch_gru_fwd_tag {};
 struct launch_gru_bwd_tag {};
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
+template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
+#ifdef EXP_GF_RT1
+template <> struct kSplitRT<launch_gru_fwd_tag> { static constexpr int value = 1; };
+#endif
+#ifdef EXP_GB_RT1
+template <> struct kSplitRT<launch_gru_bwd_tag> { static constexpr int value = 1; };
+#endif
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
 
 void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,

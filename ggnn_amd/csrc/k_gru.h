@@ -14,6 +14,9 @@
 // weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
 // full unrolling, which spills at H = 256)
 constexpr int GF_UNROLL = 2, GB_UNROLL = 2;
+// gru_bwd elementwise phases: loads of GB_GROUP row quads (x 4 arrays) in flight
+// between scheduling barriers (measured: 4 > 2 > 1; VGPRs stay within budget)
+constexpr int GB_GROUP = 4, GB_GROUP2 = 4;
 
 // ===========================================================================
 // k_gru_fwd
@@ -252,7 +255,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       }
       st_col4w<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
       st_col4w<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
-      __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
+      if ((q & (GB_GROUP - 1)) == GB_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
     }
   }
   csum += __shfl_xor(csum, 32);
@@ -301,7 +304,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
       }
       st_col4w<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
-      __builtin_amdgcn_sched_barrier(0);
+      if ((q & (GB_GROUP2 - 1)) == GB_GROUP2 - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
   rsum += __shfl_xor(rsum, 32);
