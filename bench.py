@@ -3,11 +3,12 @@
 
 Metric and config from BASELINE.json: hidden=256, v=128, e=4 edge types
 (C = 2e = 8 adjacency channels), T=5, batch 256 graphs per GPU (configs[2]).
-One "step" = one pass of the hot path over one batch already resident in HBM:
-  pack weights (fp32 -> bf16 fragments) + stage adjacency ([b,C,v,v] fp32 ->
-  bf16 + transpose) + T-step forward + full backward (dL/dh0 and all six
-  weight gradients) [+ one RCCL all-reduce of the flat gradient buffer when
-  N > 1].
+One "step" = one training step of the hot path over one batch already
+resident in HBM: pack weights (fp32 -> MFMA fragment limbs) + stage adjacency
+([b,C,v,v] fp32 -> 16-bit + transpose) + T-step forward + full backward (dL/dh0
+and all six weight gradients) [+ one RCCL all-reduce of the flat gradient
+buffer when N > 1] + the reference's optimizer update of the six variables
+(per-tensor clip_by_norm + TF1 Adam, chem_tensorflow.py:494-503).
 Weak scaling: every rank owns its own 256-graph batch; value = N*256 / t_step
 with t_step the max over ranks.
 
@@ -174,6 +175,9 @@ def main():
     dhT = torch.from_numpy(np.random.default_rng(7 + rank).standard_normal((b, v, h)).astype(np.float32)).to(dev)
     eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision)
     grads = FlatGradients(h, C, True, device=dev)
+    from ggnn_amd.dist import GRAD_ORDER
+    from ggnn_amd.optim import ClipAdam
+    opt = ClipAdam([w_d[k] for k in GRAD_ORDER], learning_rate=0.003, clamp_gradient_norm=1.0)
     gviews = dict(grads.views)
     gviews["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
     out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
@@ -189,6 +193,7 @@ def main():
         eng.forward(h0_d, pack, T, training=True, out=out, state_keep=keep)
         eng.backward(dhT, gviews)
         grads.all_reduce()
+        opt.step([grads.views[k] for k in GRAD_ORDER], grad_scale=1.0 / world)
 
     def barrier():
         if world > 1:

@@ -22,10 +22,10 @@ EXPORTED = (
     "ggnn_version", "ggnn_last_error", "ggnn_check_dims", "ggnn_workspace_bytes",
     "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
     "ggnn_set_adjacency_edges",
-    "ggnn_forward", "ggnn_backward", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
+    "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end",
 )
-NUM_KERNEL_KINDS = 8
+NUM_KERNEL_KINDS = 9
 
 
 class GGNNDims(ctypes.Structure):
@@ -83,6 +83,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_forward.argtypes = [_DP, _P, _P, _P, _I, _P, _P, _P]
         lib.ggnn_backward.restype = _I
         lib.ggnn_backward.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+        lib.ggnn_adam_step.restype = _I
+        lib.ggnn_adam_step.argtypes = [_P, _I, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                       ctypes.c_float, ctypes.c_int64, ctypes.c_float, _P, _P]
         lib.ggnn_dropout_mask.restype = _I
         lib.ggnn_dropout_mask.argtypes = [_DP, _I, _I, _P, _P]
         lib.ggnn_kernel_kind_name.restype = ctypes.c_char_p

@@ -15,6 +15,7 @@
 #include "k_gru.h"
 #include "k_prep.h"
 #include "k_prop.h"
+#include "k_optim.h"
 #include "k_wgrad.h"
 
 // ---------------------------------------------------------------------------
@@ -40,8 +41,8 @@ namespace {
 
 // ---- optional per-kernel-kind timing with HIP events (bench.py roofline)
 const char* const kKindNames[GGNN_NUM_KERNEL_KINDS] = {
-    "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad"};
-enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD };
+    "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad", "optimizer"};
+enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD, K_OPT };
 struct ProfState {
   bool on = false;
   int cap = 0, used = 0;
@@ -632,6 +633,46 @@ int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_s
   const long total = kind == 0 ? (long)c.C * c.H * c.H : (long)c.b * c.vin * c.H;
   hipLaunchKernelGGL(k_dropout_mask, dim3(grid1d(total)), dim3(256), 0, s, kind, c.C, c.H, c.b, c.vin, t,
                      kind == 0 ? c.edrop : c.sdrop, mask);
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate, float beta1, float beta2,
+                   float epsilon, float clip_norm, int64_t step, float grad_scale, float* scratch,
+                   ggnn_stream_t stream) {
+  if (!tensors || !scratch) return fail(GGNN_EINVAL, "adam_step: NULL pointer");
+  if (count < 1 || count > GGNN_OPT_MAXT)
+    return fail(GGNN_EINVAL, "adam_step: count must be in 1.." + std::to_string(GGNN_OPT_MAXT));
+  if (step < 1) return fail(GGNN_EINVAL, "adam_step: step counts from 1");
+  if (!(clip_norm > 0.f)) return fail(GGNN_EINVAL, "adam_step: clip_norm must be > 0");
+  OptArgs a;
+  memset(&a, 0, sizeof(a));
+  a.count = count;
+  long off = 0;
+  for (int i = 0; i < count; ++i) {
+    const ggnn_adam_tensor& t = tensors[i];
+    if (!t.param || !t.grad || !t.m || !t.v || t.n < 1) return fail(GGNN_EINVAL, "adam_step: bad tensor entry");
+    a.t[i] = OptTensor{t.param, t.grad, t.m, t.v, (long)t.n};
+    a.begin[i] = off;
+    off += t.n;
+  }
+  a.begin[count] = off;
+  // TF1 Adam folds both bias corrections into the step size
+  const double b1t = std::pow((double)beta1, (double)step), b2t = std::pow((double)beta2, (double)step);
+  a.lr_t = (float)(learning_rate * std::sqrt(1.0 - b2t) / (1.0 - b1t));
+  a.gscale = grad_scale;
+  a.clip = clip_norm;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = epsilon;
+  hipStream_t s = (hipStream_t)stream;
+  Prof p(K_OPT, s);
+  HIPCHK(hipMemsetAsync(scratch, 0, (size_t)count * 4, s));
+  long maxn = 1;
+  for (int i = 0; i < count; ++i) maxn = std::max<long>(maxn, a.t[i].n);
+  const dim3 grid((unsigned)std::min<long>(256, (maxn + 255) / 256), (unsigned)count);
+  hipLaunchKernelGGL(k_opt_sqnorm, grid, dim3(256), 0, s, a, scratch);
+  hipLaunchKernelGGL(k_opt_adam, grid, dim3(256), 0, s, a, (const float*)scratch);
   LAUNCHCHK();
   return GGNN_OK;
 }

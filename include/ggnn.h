@@ -151,6 +151,27 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
                   float* d_candidate_kernel, float* d_candidate_bias,
                   ggnn_stream_t stream);
 
+/* The reference's optimizer step for the path's variables
+ * (chem_tensorflow.py:494-503): every gradient scaled by grad_scale (1/N for
+ * an N-rank data-parallel mean), clipped per tensor with tf.clip_by_norm
+ * (g * clip_norm / max(||g||_2, clip_norm), params['clamp_gradient_norm']),
+ * then one tf.compat.v1.train.AdamOptimizer update (learning_rate,
+ * beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8 in the reference):
+ *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
+ *   p -= lr sqrt(1-b2^step)/(1-b1^step) m / (sqrt(v) + eps),  step >= 1.
+ * scratch: device float[count].  Two HBM-bound launches. */
+typedef struct ggnn_adam_tensor {
+  float* param;
+  const float* grad;
+  float* m;  /* first-moment slot, zero-initialised by the caller */
+  float* v;  /* second-moment slot, zero-initialised by the caller */
+  int64_t n;
+} ggnn_adam_tensor;
+#define GGNN_ADAM_MAX_TENSORS 16
+int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate,
+                   float beta1, float beta2, float epsilon, float clip_norm,
+                   int64_t step, float grad_scale, float* scratch, ggnn_stream_t stream);
+
 /* Materialise a dropout keep-mask (1 = kept, 0 = dropped) exactly as the
  * kernels apply it, for verification: kind 0 = edge-weight mask of timestep t
  * ([C][h][h] bytes), kind 1 = state mask of timestep t ([b][v][h] bytes). */
@@ -159,7 +180,7 @@ int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_s
 /* Optional per-kernel timing (HIP events around every launch of the library
  * on the launch's stream), used by bench.py for the roofline.  Not for use
  * under graph capture.  total_ms / launches: arrays of GGNN_NUM_KERNEL_KINDS. */
-#define GGNN_NUM_KERNEL_KINDS 8
+#define GGNN_NUM_KERNEL_KINDS 9
 const char* ggnn_kernel_kind_name(int kind);
 int ggnn_profile_begin(int max_launches);
 int ggnn_profile_end(double* total_ms, int* launches);

@@ -439,3 +439,29 @@ def test_drop_in_model_compact_adjacency_feed():
         outs.append(m.compute_final_node_representations(torch.from_numpy(h0.astype(np.float32)).to(m.device))
                     .detach().cpu().numpy())
     assert np.array_equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------------------ optimizer
+def test_clip_adam_matches_tf1_semantics():
+    """ggnn_adam_step: tf.clip_by_norm per tensor + TF1 Adam, 3 steps, against
+    the float64 oracle (chem_tensorflow.py:494-503)."""
+    torch = _torch()
+    from ggnn_amd.dist import grad_shapes
+    from ggnn_amd.optim import ClipAdam
+    rng = np.random.default_rng(0)
+    shapes = list(grad_shapes(128, 4).values())
+    p0 = [rng.standard_normal(s).astype(np.float32) * 0.1 for s in shapes]
+    dev = torch.device("cuda", 0)
+    params = [torch.from_numpy(x.copy()).to(dev) for x in p0]
+    opt = ClipAdam(params, learning_rate=0.003, clamp_gradient_norm=1.0)
+    ref_p = [x.astype(np.float64) for x in p0]
+    ref_m = [np.zeros_like(x) for x in ref_p]
+    ref_v = [np.zeros_like(x) for x in ref_p]
+    for t in range(1, 4):
+        # tensor norms on both sides of the clip (small biases stay unclipped)
+        grads = [rng.standard_normal(s).astype(np.float32) * (0.01 if len(s) == 1 else 0.5) for s in shapes]
+        opt.step([torch.from_numpy(g).to(dev) for g in grads], grad_scale=0.5)
+        O.adam_step(ref_p, grads, ref_m, ref_v, t, lr=0.003, clip_norm=1.0, grad_scale=0.5)
+    torch.cuda.synchronize()
+    for got, ref in zip(params, ref_p):
+        assert np.abs(got.cpu().numpy() - ref).max() <= 1e-6

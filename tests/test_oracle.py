@@ -176,3 +176,18 @@ def test_dropout_backward_matches_finite_differences():
             else:
                 num[idx] = (loss({**w, key: p}, h0) - loss({**w, key: m}, h0)) / (2 * eps)
         assert np.abs(num - g[key]).max() <= 1e-7 * max(1.0, np.abs(num).max()), key
+
+
+# ---------------------------------------------------------------- optimizer
+def test_clip_by_norm_and_adam_known_answer():
+    # clip_by_norm: ||(3, 4)|| = 5 > 1 -> (0.6, 0.8); below the clip it is the identity
+    np.testing.assert_allclose(O.clip_by_norm(np.array([3.0, 4.0]), 1.0), [0.6, 0.8])
+    np.testing.assert_allclose(O.clip_by_norm(np.array([0.3, 0.4]), 1.0), [0.3, 0.4])
+    # TF1 Adam, first step: m = 0.1 g, v = 0.001 g^2, lr_t = lr sqrt(0.001)/0.1
+    # -> p -= lr * g/|g| (1 + O(eps)) element-wise
+    p, g = [np.array([1.0, -2.0])], [np.array([0.3, -0.4])]
+    m, v = [np.zeros(2)], [np.zeros(2)]
+    O.adam_step(p, g, m, v, 1, lr=0.01)
+    np.testing.assert_allclose(p[0], [1.0 - 0.01, -2.0 + 0.01], rtol=1e-6)
+    np.testing.assert_allclose(m[0], [0.03, -0.04])
+    np.testing.assert_allclose(v[0], [0.3 ** 2 * 1e-3, 0.4 ** 2 * 1e-3])
