@@ -95,12 +95,17 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   // wait of pass B cover it.
   // (At RT = 4 keeping r live through pass B spills: store early there.)
   constexpr bool DEFER = RT <= 2;
+  // h (fp32) of this lane's elements, kept in registers for the blend (the h
+  // image is overwritten by r*h); at RT = 4 the blend re-reads it instead
+  float hv[DEFER ? RT : 1][16];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     float rh[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      rh[r] = ar[rt][r] * bld(rh_in, vo, (rt * 32 + acc_row0(r)) * H * 4);
+      const float hx = bld(rh_in, vo, (rt * 32 + acc_row0(r)) * H * 4);
+      if constexpr (DEFER) hv[rt][r] = hx;
+      rh[r] = ar[rt][r] * hx;
       img_put<PREC, HCH>(h_hi, h_lo, rt * 32 + acc_row(r, hh), n, rh[r]);
     }
     if constexpr (!DEFER) {
@@ -155,7 +160,9 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       const int so = (rt * 32 + acc_row0(r)) * H * 4;
       const float cc = tanh_f(ac[rt][r]);
       const float u = au[rt][r];
-      const float hprev = bld(rh_in, vo, so);
+      float hprev;
+      if constexpr (DEFER) hprev = hv[rt][r];
+      else hprev = bld(rh_in, vo, so);
       float hn = u * hprev + (1.0f - u) * cc;
       if (dr.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
         if ((r & 3) == 0) {
