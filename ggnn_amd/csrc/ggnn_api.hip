@@ -600,24 +600,48 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   hipStream_t s = (hipStream_t)stream;
   const PackL L = pack_layout(c);
   const int H = c.H;
-  for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
-    launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, s,
-                c.edrop, t);  // MT: Bmat = W_c
-    launch_pack(c.prec != PREC_BF16, W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, s,
-                c.edrop, t);  // dh: Bmat = W_c^T
-  }
-  launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, s);
-  launch_pack(c.prec != PREC_BF16, Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, s);
-  launch_pack(c.prec != PREC_BF16, Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, s);   // Bmat = Wc   [2H][H]
-  launch_pack(c.prec != PREC_BF16, Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, s);  // Bmat = Wc^T [H][2H]
-  {
+  PackJobs a;
+  memset(&a, 0, sizeof(a));
+  a.dr = c.edrop;
+  int nb = 0;
+  auto flush = [&]() {
+    if (!a.count) return;
+    a.blk_begin[a.count] = nb;
     Prof p(K_PACK, s);
-    const float* bsrc = (c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr;
-    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d((long)c.C * H)), dim3(256), 0, s, bsrc, P<float>(pack, L.beta),
-                       (long)c.C * H);
-    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(2 * H)), dim3(256), 0, s, bg, P<float>(pack, L.bg), (long)2 * H);
-    hipLaunchKernelGGL(k_copy_f32, dim3(grid1d(H)), dim3(256), 0, s, bc, P<float>(pack, L.bc), (long)H);
+    if (c.prec != PREC_BF16) hipLaunchKernelGGL(k_pack_multi<true>, dim3(nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pack_multi<false>, dim3(nb), dim3(256), 0, s, a);
+    a.count = 0;
+    nb = 0;
+  };
+  auto job = [&](const float* S, int ldS, long sS, int K, int N, int trans, void* out, long sO, long lo, int batch,
+                 int t, int drop) {
+    if (a.count == PACK_MAXJ) flush();  // (long T under edge dropout)
+    PackJob& J = a.j[a.count];
+    J.S = S; J.out = (u16*)out; J.sS = sS; J.sO = sO; J.lo_off = lo;
+    J.total = (long)batch * (N / 32) * (K / 16) * 64;
+    J.ldS = ldS; J.K = K; J.N = N; J.trans = trans; J.t = t; J.drop = drop; J.copy = 0;
+    a.blk_begin[a.count++] = nb;
+    nb += (int)((J.total + 255) / 256);
+  };
+  auto copy = [&](const float* S, float* out, long n) {
+    if (a.count == PACK_MAXJ) flush();
+    PackJob& J = a.j[a.count];
+    J.S = S; J.out = (u16*)out; J.total = n; J.copy = 1;
+    a.blk_begin[a.count++] = nb;
+    nb += (int)((n + 255) / 256);
+  };
+  for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
+    job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
+    job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
   }
+  job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
+  job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
+  job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
+  job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
+  copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
+  copy(bg, P<float>(pack, L.bg), 2L * H);
+  copy(bc, P<float>(pack, L.bc), (long)H);
+  flush();
   LAUNCHCHK();
   return GGNN_OK;
 }

@@ -285,3 +285,52 @@ __global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, u16* 
   }
   deg[tile * V + threadIdx.x] = to_limb<F16>(s);
 }
+
+// ---- all weight packs of one ggnn_pack_weights call in ONE launch: a job
+// table of k_pack_B problems (and fp32 copies for the biases); block b runs
+// job j with blk_begin[j] <= b < blk_begin[j+1]
+#define PACK_MAXJ 24
+struct PackJob {
+  const float* S;
+  u16* out;      // copy jobs: float* destination
+  long sS, sO, lo_off, total;  // total: fragment-lanes (pack) or elements (copy)
+  int ldS, K, N, trans, t, drop, copy;
+};
+struct PackJobs {
+  PackJob j[PACK_MAXJ];
+  int blk_begin[PACK_MAXJ + 1];
+  int count;
+  Drop dr;
+};
+template <bool F16>
+__global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
+  int ji = 0;
+  while (ji + 1 < a.count && a.blk_begin[ji + 1] <= (int)blockIdx.x) ++ji;
+  const PackJob& J = a.j[ji];
+  const long q = (long)(blockIdx.x - a.blk_begin[ji]) * 256 + threadIdx.x;
+  if (q >= J.total) return;
+  if (J.copy) {
+    ((float*)J.out)[q] = J.S ? J.S[q] : 0.0f;
+    return;
+  }
+  const int per = (J.N / 32) * (J.K / 16) * 64;  // fragment-lanes per matrix
+  const int mat = (int)(q / per), r = (int)(q % per);
+  const float* Sb = J.S + J.sS * mat;
+  u16* ob = J.out + J.sO * mat;
+  const int lane = r & 63, fi = r >> 6;
+  const int nks = J.K / 16;
+  const int ks = fi % nks, strip = fi / nks;
+  const int n = strip * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = J.trans ? Sb[(long)n * J.ldS + k0 + e] : Sb[(long)(k0 + e) * J.ldS + n];
+  if (J.drop) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int wi = J.trans ? n : k0 + e, wj = J.trans ? k0 + e : n;
+      x[e] = drop_apply(a.dr, u4_get(edge_words(a.dr, mat, wi, wj, J.t), wi & 3), x[e]);
+    }
+  }
+  *(uint4*)(ob + (size_t)r * 8) = pk8<F16>(x);
+  *(uint4*)(ob + J.lo_off + (size_t)r * 8) = pk8_lo<F16>(x);
+}

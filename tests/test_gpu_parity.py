@@ -465,3 +465,15 @@ def test_clip_adam_matches_tf1_semantics():
     torch.cuda.synchronize()
     for got, ref in zip(params, ref_p):
         assert np.abs(got.cpu().numpy() - ref).max() <= 1e-6
+
+
+def test_edge_dropout_long_unroll_packs_in_several_launches():
+    """T = 12 timesteps under edge dropout: 2T + 7 pack jobs exceed one launch's
+    job table; the packs must still be the per-timestep masked weights."""
+    A, h0, w = _case(2, 20, 128, 4, seed=31)
+    dhT = np.random.default_rng(2).standard_normal(h0.shape).astype(np.float32)
+    dr = dict(edge_keep=0.8, state_keep=1.0, seed=77)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, 12, dropout=dr)
+    got = _run_dropout(A, h0, w, 12, "fp32", dr, dhT)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
