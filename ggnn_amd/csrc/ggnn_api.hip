@@ -691,10 +691,10 @@ int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_ra
   a.eps = epsilon;
   hipStream_t s = (hipStream_t)stream;
   Prof p(K_OPT, s);
-  HIPCHK(hipMemsetAsync(scratch, 0, (size_t)count * 4, s));
   long maxn = 1;
   for (int i = 0; i < count; ++i) maxn = std::max<long>(maxn, a.t[i].n);
-  const dim3 grid((unsigned)std::min<long>(256, (maxn + 255) / 256), (unsigned)count);
+  // scratch holds count * OPT_BLOCKS per-block partial norms
+  const dim3 grid((unsigned)std::min<long>(GGNN_ADAM_SCRATCH_PER_TENSOR, (maxn + 255) / 256), (unsigned)count);
   hipLaunchKernelGGL(k_opt_sqnorm, grid, dim3(256), 0, s, a, scratch);
   hipLaunchKernelGGL(k_opt_adam, grid, dim3(256), 0, s, a, (const float*)scratch);
   LAUNCHCHK();

@@ -37,13 +37,22 @@ __global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sq + blockIdx.y, red[0] + red[1] + red[2] + red[3]);
+  // per-block partial (no atomics, no zeroing): sq[tensor * gridDim.x + block]
+  if (threadIdx.x == 0) sq[blockIdx.y * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 __global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __restrict__ sq) {
   const OptTensor& T = a.t[blockIdx.y];
+  __shared__ float tot;
+  if (threadIdx.x < 64) {  // this tensor's squared norm from the sqnorm launch's partials
+    float x = 0.f;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 64) x += sq[blockIdx.y * gridDim.x + i];
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    if (threadIdx.x == 0) tot = x;
+  }
+  __syncthreads();
   // tf.clip_by_norm: t * clip / max(l2norm, clip)
-  const float scale = a.gscale * a.clip / fmaxf(sqrtf(sq[blockIdx.y]), a.clip);
+  const float scale = a.gscale * a.clip / fmaxf(sqrtf(tot), a.clip);
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < T.n; e += (long)gridDim.x * blockDim.x) {
     const float g = T.g[e] * scale;
     const float m = a.b1 * T.m[e] + (1.0f - a.b1) * g;

@@ -21,6 +21,7 @@ class AdamTensor(ctypes.Structure):
 
 
 MAX_TENSORS = 16
+SCRATCH_PER_TENSOR = 256   # GGNN_ADAM_SCRATCH_PER_TENSOR
 
 
 class ClipAdam:
@@ -45,7 +46,7 @@ class ClipAdam:
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
         self.t = 0
-        self._scratch = torch.zeros(MAX_TENSORS, dtype=torch.float32, device=self.params[0].device)
+        self._scratch = torch.zeros(MAX_TENSORS * SCRATCH_PER_TENSOR, dtype=torch.float32, device=self.params[0].device)
         self._lib = _lib.load()
 
     @torch.no_grad()

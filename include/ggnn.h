@@ -159,7 +159,9 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
  * beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8 in the reference):
  *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
  *   p -= lr sqrt(1-b2^step)/(1-b1^step) m / (sqrt(v) + eps),  step >= 1.
- * scratch: device float[count].  Two HBM-bound launches. */
+ * scratch: device float[count * GGNN_ADAM_SCRATCH_PER_TENSOR].  Two
+ * HBM-bound launches (per-tensor norms, then the update). */
+#define GGNN_ADAM_SCRATCH_PER_TENSOR 256
 typedef struct ggnn_adam_tensor {
   float* param;
   const float* grad;
