@@ -146,6 +146,9 @@ def main():
     ap.add_argument("--dropout-keep", type=float, default=0.9,
                     help="keep probability of the dropout-on line (graph_state_dropout_keep_prob)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (default nccl = RCCL; gloo only to rehearse "
+                         "several ranks on one GPU)")
     ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
                     help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
                          "parity mode); fp16 / bf16: single 16-bit MFMA operands (reduced precision)")
@@ -159,9 +162,10 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ggnn_oracle as O  # synthetic input generator; not timed
 
-    rank, world, local = init_from_env()
+    rank, world, local = init_from_env(args.dist_backend)
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    local = local % max(torch.cuda.device_count(), 1)  # (ranks sharing a GPU: the gloo rehearsal only)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
