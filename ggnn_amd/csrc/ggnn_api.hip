@@ -297,12 +297,6 @@ struct launch_gru_fwd_tag {};
 struct launch_gru_bwd_tag {};
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
 template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
-#ifdef EXP_GF_RT1
-template <> struct kSplitRT<launch_gru_fwd_tag> { static constexpr int value = 1; };
-#endif
-#ifdef EXP_GB_RT1
-template <> struct kSplitRT<launch_gru_bwd_tag> { static constexpr int value = 1; };
-#endif
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
 
 void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,

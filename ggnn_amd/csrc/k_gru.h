@@ -60,13 +60,9 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   }
   // ---- pass A over k in [0, 2H): x rows then h rows of Wg
   auto ldg = [&](int k) {
-#ifdef EXP_GF_W0
-    k = k & 1;
-#endif
     return F4{frag_ld(Wgp, ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, ns, k, KSG, lane) : frag{},
               frag_ld(Wgp, NS + ns, k, KSG, lane), SPLIT ? frag_ld(Wgp + wlo_g, NS + ns, k, KSG, lane) : frag{}};
   };
-#ifndef EXP_GF_NO_PASSA
   b_pipeline<KSG, 2, GF_UNROLL>(ldg, [&](int k, const F4& w) {
     const char* ih = (k < KS) ? x_hi : h_hi;
     const char* il = (k < KS) ? x_lo : h_lo;
@@ -79,7 +75,6 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(au[rt], ah, al, w.c, w.d);
     }
   });
-#endif
   const rsrc_t rh_in = mkrsrc(hf + row0 * H, R * H * 4);
   const int vo = (4 * hh * H + n) * 4;
 #pragma unroll
@@ -131,13 +126,9 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     for (int rt = 0; rt < RT; ++rt) ac[rt] = splat(b0);
   }
   auto ldc = [&](int ks) {
-#ifdef EXP_GF_W0
-    ks = ks & 1;
-#endif
     return F4{frag_ld(Wcp, ns, ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, ks, KSG, lane) : frag{},
               frag_ld(Wcp, ns, KS + ks, KSG, lane), SPLIT ? frag_ld(Wcp + wlo_c, ns, KS + ks, KSG, lane) : frag{}};
   };
-#ifndef EXP_GF_NO_PASSB
   b_pipeline<KS, 2, GF_UNROLL>(ldc, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -148,7 +139,6 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(ac[rt], qh, ql, w.c, w.d);
     }
   });
-#endif
   // ---- blend + outputs
   const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
   uint4 dw = make_uint4(0, 0, 0, 0);
@@ -278,7 +268,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
               frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
   };
-#ifndef EXP_GB_NO_P1
   b_pipeline<KS, 2, GB_UNROLL>(ld1, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -288,7 +277,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
   });
-#endif
   __syncthreads();  // dzc reads done
 
   // ---- phase 2: dh (into a2), the r half of dzg
@@ -323,7 +311,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
               frag_ld(WgTp, NS + ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
   };
-#ifndef EXP_GB_NO_P2
   b_pipeline<2 * KS, 2, GB_UNROLL>(ld2, [&](int ks, const F4& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -333,7 +320,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
   });
-#endif
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {

@@ -71,10 +71,8 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     };
     // measured (config 3): the ring pays in the 3-product split mode, the
     // fully unrolled direct loop in the single-product modes
-#ifndef EXP_NO_MT
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
-#endif
     __syncthreads();  // S1: A_c visible
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
@@ -85,10 +83,8 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
       for (int it = 0; it < VT; ++it) {
         const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
         const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
-#ifndef EXP_NO_AGG
         mma_xa<PREC>(accx[it], a0, mh0, ml0);
         mma_xa<PREC>(accx[it], a1, mh1, ml1);
-#endif
       }
     }
     __syncthreads();  // S2: A_c reads done
@@ -191,13 +187,11 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
 #pragma unroll
     for (int jt = 0; jt < VT; ++jt) {
       f32x16 am = splat(0.f);
-#ifndef EXP_NO_PHASE_A
 #pragma unroll
       for (int s = 0; s < KV; ++s) {
         const frag b = lds_frag(abuf, SA::off(jt * 32 + l32, 2 * s + hh));
         mma_xb<PREC>(am, dxh[s], dxl[s], b);
       }
-#endif
       const int j = jt * 32 + l32;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -210,11 +204,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         dq[jt][q] = quad_transpose4(p0, p1, l32 & 3);
       }
     }
-#ifndef EXP_NO_DBETA
     if (dbp) {
-#else
-    if (false) {
-#endif
       // dbeta_c[n] = sum_i dX[i][n] deg_c[i] as one more MFMA product: B[i][*] =
       // deg_c[i] (exact integers), every output column holds the sum.  Per-graph
       // partials [b][C][H] (no atomics); reduced over graphs after the last step.
@@ -237,7 +227,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     const u16* wt = WTp + (size_t)c * H * H;
     const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
     const int vm = (int)((((long)ns * 32 + 4 * hh + (l32 & 3)) * N + rowg + 4 * (l32 >> 2)) * 2);
-#ifndef EXP_NO_PHASE_B
     auto ldb = [&](int ks) {
       return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
     };
@@ -251,12 +240,10 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       }
     };
     b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)
-#endif
     // dM_c^T -> HBM [c][n][N] (weight-gradient operand).  Issued after the last
     // weight-fragment wait of the channel: vmcnt is in order, so a store ahead of
     // a load would make that load's wait cover the store too.  The stores then
     // drain during the next channel's phase a, which has no vector-memory loads.
-#ifndef EXP_NO_DMT
     if (dMT) {
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt)
@@ -264,7 +251,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         for (int q = 0; q < 4; ++q)
           __builtin_amdgcn_raw_buffer_store_b64(dq[jt][q], rdm, vm + jt * 64, 8 * q * N * 2, kNT);
     }
-#endif
     __syncthreads();  // S2: dM image reads done, A_{c+1} staged
   }
   const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
