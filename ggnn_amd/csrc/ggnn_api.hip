@@ -477,6 +477,7 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   }
   constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
+  a.H = (int)H;
   if (big) {
     // one workgroup per CU (128 KiB LDS ring): the largest K chunk that still
     // gives >= 7/8 of the CUs a tile-chunk

@@ -312,6 +312,15 @@ DEV void st_col4(ActT<PREC>* dst, float a, float b, float c, float d) {
   else *(uint2*)dst = make_uint2(pk<Prec<PREC>::f16>(a, b), pk<Prec<PREC>::f16>(c, d));
 }
 
+// Weight-gradient operand layout.  An operand is an [H][N] array (hidden
+// index n, node row k) stored in K-blocks of 32 rows: block k>>5 holds
+// [H][32], so element (n, k) sits at wg_off(n, k, H).  A weight-gradient K
+// slice (all H rows x 32 node rows) is then one contiguous 16 KiB span
+// instead of H 64-byte pieces 2N bytes apart, which all fell into the same
+// L2 sets (k_wgrad256: 0.42 -> 0.32 ms/step at config 3), and a 4-row store
+// of 8 lanes fills one 64-byte row.  Needs N % 32 == 0 (V is 32, 64 or 128).
+DEV long wg_off(int n, long k, int H) { return ((k >> 5) * H + n) * 32 + (k & 31); }
+
 // Weight-gradient operands (X^T, h^T, (r*h)^T, dzc^T, dzg^T, dM^T) are only
 // summed into the weight gradients, where rounding errors do not compound over
 // timesteps: they are stored as ONE 16-bit limb in every mode (f16 unless the

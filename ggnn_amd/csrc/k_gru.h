@@ -107,7 +107,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       if (rhT_out) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, rh[4 * q], rh[4 * q + 1],
+          st_col4w<PREC>(rhT_out + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, rh[4 * q], rh[4 * q + 1],
                          rh[4 * q + 2], rh[4 * q + 3]);
       }
       if (r_out) {
@@ -174,13 +174,13 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     if (DEFER && rhT_out) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4w<PREC>(rhT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, au[rt][4 * q], au[rt][4 * q + 1],
+        st_col4w<PREC>(rhT_out + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, au[rt][4 * q], au[rt][4 * q + 1],
                        au[rt][4 * q + 2], au[rt][4 * q + 3]);
     }
     if (hT_out) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4w<PREC>(hT_out + (long)n * N + row0 + rt * 32 + 8 * q + 4 * hh, ac[rt][4 * q], ac[rt][4 * q + 1],
+        st_col4w<PREC>(hT_out + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, ac[rt][4 * q], ac[rt][4 * q + 1],
                        ac[rt][4 * q + 2], ac[rt][4 * q + 3]);
     }
   }
@@ -226,7 +226,8 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   const rsrc_t pd = mkrsrc(delta + tb0, tbytes), ph = mkrsrc(hf + tb0, tbytes), pr = mkrsrc(rin + tb0, tbytes),
                pu = mkrsrc(uin + tb0, tbytes), pc = mkrsrc(cin + tb0, tbytes);
   const int vo = (4 * hh * H + n) * 4;
-  const long tcol = (long)n * N + row0 + 4 * hh;
+  const long tcol = (long)n * N + row0 + 4 * hh;   // dX^T (prop_bwd's operand)
+  const long twg = wg_off(n, row0 + 4 * hh, H);   // dzc^T / dzg^T (weight-gradient operands)
 
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
@@ -250,8 +251,8 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, H + n, zu[i]);  // K >= H: not read by product 1
       }
-      st_col4w<PREC>(dzcT + tcol + rt * 32 + 8 * q, dz[0], dz[1], dz[2], dz[3]);
-      st_col4w<PREC>(dzgT + tcol + (long)H * N + rt * 32 + 8 * q, zu[0], zu[1], zu[2], zu[3]);
+      st_col4w<PREC>(dzcT + twg + rt * 32 * H + 8 * q, dz[0], dz[1], dz[2], dz[3]);
+      st_col4w<PREC>(dzgT + twg + (long)H * N + rt * 32 * H + 8 * q, zu[0], zu[1], zu[2], zu[3]);
       if ((q & (GB_GROUP - 1)) == GB_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPR budget)
     }
   }
@@ -298,7 +299,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         rsum += zr[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
       }
-      st_col4w<PREC>(dzgT + tcol + rt * 32 + 8 * q, zr[0], zr[1], zr[2], zr[3]);
+      st_col4w<PREC>(dzgT + twg + rt * 32 * H + 8 * q, zr[0], zr[1], zr[2], zr[3]);
       if ((q & (GB_GROUP2 - 1)) == GB_GROUP2 - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }

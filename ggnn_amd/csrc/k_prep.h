@@ -203,7 +203,8 @@ __global__ void k_sum_graphs(const float* __restrict__ part, float* __restrict__
 }
 
 // Training-forward staging of h0 in one pass: h0 [b][vin][H] fp32 -> hf [N][H]
-// fp32 (pad rows zero), optional hb (16-bit limbs), and hT [H][N] (16-bit
+// fp32 (pad rows zero), optional hb (16-bit limbs), and hT [H][N] (16-bit,
+// wg_off layout;
 // limbs, the weight-gradient operand of timestep 0).  64x64 tiles via LDS.
 template <bool F16>
 __global__ void __launch_bounds__(256) k_stage_h0(const float* __restrict__ h0, int vin, int V, float* __restrict__ hf,
@@ -227,7 +228,7 @@ __global__ void __launch_bounds__(256) k_stage_h0(const float* __restrict__ h0, 
   __syncthreads();
   for (int q = threadIdx.x; q < 64 * 64; q += 256) {
     const int j = q / 64, i = q % 64;
-    if (r0 + i < N) hT[(long)(c0 + j) * N + r0 + i] = to_limb<F16>(t[i][j]);
+    if (r0 + i < N) hT[wg_off(c0 + j, r0 + i, H)] = to_limb<F16>(t[i][j]);
   }
 }
 

@@ -98,7 +98,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     for (int it = 0; it < VT; ++it)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        st_col4w<PREC>(XT + (long)n * N + rowg + it * 32 + 8 * q + 4 * hh, accx[it][4 * q], accx[it][4 * q + 1],
+        st_col4w<PREC>(XT + wg_off(n, rowg + it * 32 + 4 * hh, H) + 8 * q, accx[it][4 * q], accx[it][4 * q + 1],
                        accx[it][4 * q + 2], accx[it][4 * q + 3]);
   }
   // ---- X row-major through LDS (the h images are free after the last S2)
@@ -226,7 +226,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
     const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
-    const int vm = (int)((((long)ns * 32 + 4 * hh + (l32 & 3)) * N + rowg + 4 * (l32 >> 2)) * 2);
+    const int vm = (int)(wg_off(ns * 32 + 4 * hh + (l32 & 3), rowg + 4 * (l32 >> 2), H) * 2);
     auto ldb = [&](int ks) {
       return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
     };
@@ -249,7 +249,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       for (int jt = 0; jt < VT; ++jt)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          __builtin_amdgcn_raw_buffer_store_b64(dq[jt][q], rdm, vm + jt * 64, 8 * q * N * 2, kNT);
+          __builtin_amdgcn_raw_buffer_store_b64(dq[jt][q], rdm, vm + jt * 64 * H, 8 * q * 64, kNT);
     }
     __syncthreads();  // S2: dM image reads done, A_{c+1} staged
   }

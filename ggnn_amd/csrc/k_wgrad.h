@@ -1,7 +1,8 @@
 // k_wgrad.h -- weight gradients as one grouped split-K "NT" GEMM launch:
 //   out[m][n] += sum_{t < T} sum_{k in chunk} P_t[m][k] * Q_t[n][k]
 // P_t / Q_t are the transposed activations saved per timestep ([M][K] and
-// [N][K], K = the b*V node rows, contiguous).  Problems (reference autodiff,
+// [N][K], K = the b*V node rows), each a stack of [H][K] arrays in the
+// K-blocked wg_off layout (ggnn_common.h).  Problems (reference autodiff,
 // chem_tensorflow.py:496):
 //   d gates_kernel     = [X | h]^T  dzg        d candidate_kernel = [X | r*h]^T dzc
 //   d edge_weights[c]  = h^T dM_c
@@ -24,6 +25,7 @@ struct WgProb {
 struct WgArgs {
   WgProb p[WG_MAXP];
   int nprob, nchunks, KC;
+  int H;  // rows of one operand array (wg_off layout); ldP / ldQ hold its N
 };
 
 template <int BK, int PREC>
@@ -48,7 +50,7 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
   constexpr int RPB = 256 / (BK * 2);        // tile rows per 256-B LDS bank row
   auto soff = [&](int row, int ch) { return row * BK * 2 + ((ch ^ ((row / RPB) & (CH - 1))) << 4); };
 
-  const int kits = args.KC / BK, nit = kits * pr.T;
+  const int kits = args.KC / BK, nit = kits * pr.T, H = args.H;
   const long kbase = (long)chunk * args.KC;
   const Act* Pb = (const Act*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
   const Act* Qb = (const Act*)pr.Q + (long)bi * pr.sQb;
@@ -67,8 +69,9 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
       const int q = tid + p * 256, row = q / CH, ch = q % CH;
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
-        rp[p][e] = *(const V4*)(P + (long)(m0 + row) * pr.ldP + k0 + ch * 8 + 4 * e);
-        rq[p][e] = *(const V4*)(Q + (long)(n0 + row) * pr.ldQ + k0 + ch * 8 + 4 * e);
+        const int mr = m0 + row, nr = n0 + row;
+        rp[p][e] = *(const V4*)(P + (long)(mr / H) * H * pr.ldP + wg_off(mr % H, k0 + ch * 8 + 4 * e, H));
+        rq[p][e] = *(const V4*)(Q + (long)(nr / H) * H * pr.ldQ + wg_off(nr % H, k0 + ch * 8 + 4 * e, H));
       }
     }
   };
@@ -205,14 +208,16 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   auto stage = [&](int it, char* bp, char* bq) {
     const int t = it / kits;
     const long k0 = kbase + (long)(it % kits) * BK;
-    const u16* P = Pb + (long)t * pr.stepP + k0;
-    const u16* Q = Qb + (long)t * pr.stepQ + k0;
+    // wg_off layout at H = 256: the slice is one contiguous [256][32] block of
+    // the (m0 / 256)-th [H][N] array
+    const u16* P = Pb + (long)t * pr.stepP + (long)(m0 >> 8) * 256 * pr.ldP + (k0 >> 5) * 8192;
+    const u16* Q = Qb + (long)t * pr.stepQ + (long)(n0 >> 8) * 256 * pr.ldQ + (k0 >> 5) * 8192;
 #pragma unroll
     for (int g = 0; g < GPW; ++g) {
       const int qb = (g * 8 + wv) * 64;  // first 16-B slot of this wave-instruction
       const int q = qb + lane, row = q / CH, pc = q % CH, lc = pc ^ ((row >> 2) & 3);
-      glds16_asm(P + (long)(m0 + row) * pr.ldP + lc * 8, bp + qb * 16);
-      glds16_asm(Q + (long)(n0 + row) * pr.ldQ + lc * 8, bq + qb * 16);
+      glds16_asm(P + row * 32 + lc * 8, bp + qb * 16);
+      glds16_asm(Q + row * 32 + lc * 8, bq + qb * 16);
     }
   };
   f32x16 acc[4][2];
