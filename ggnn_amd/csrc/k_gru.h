@@ -226,8 +226,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   const rsrc_t pd = mkrsrc(delta + tb0, tbytes), ph = mkrsrc(hf + tb0, tbytes), pr = mkrsrc(rin + tb0, tbytes),
                pu = mkrsrc(uin + tb0, tbytes), pc = mkrsrc(cin + tb0, tbytes);
   const int vo = (4 * hh * H + n) * 4;
-  const long tcol = (long)n * N + row0 + 4 * hh;   // dX^T (prop_bwd's operand)
-  const long twg = wg_off(n, row0 + 4 * hh, H);   // dzc^T / dzg^T (weight-gradient operands)
+  const long twg = wg_off(n, row0 + 4 * hh, H);  // dX^T, dzc^T, dzg^T: K-blocked [H][N] arrays
 
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
@@ -326,7 +325,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      st_col4<PREC>(dXT + tcol + rt * 32 + 8 * q, a1[rt][4 * q], a1[rt][4 * q + 1], a1[rt][4 * q + 2],
+      st_col4<PREC>(dXT + twg + rt * 32 * H + 8 * q, a1[rt][4 * q], a1[rt][4 * q + 1], a1[rt][4 * q + 2],
                      a1[rt][4 * q + 3]);
 #pragma unroll
     for (int r = 0; r < 16; ++r) bst(pdo, a2[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);

@@ -158,7 +158,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   frag dxh[KV], dxl[KV];
 #pragma unroll
   for (int s = 0; s < KV; ++s) {
-    const Act* p = dXT + (long)n * N + rowg + 16 * s + 8 * hh;
+    const Act* p = dXT + wg_off(n, rowg + 16 * s + 8 * hh, H);  // K-blocked (ggnn_common.h)
     if constexpr (SPLIT) {
       const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
       const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
