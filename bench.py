@@ -125,6 +125,99 @@ def adjacency_feed_costs(eng, b, v, E, dev, reps=5):
             "dense_in_hbm_ms": ms_dense_dev, "dense_from_host_ms": ms_dense_h2d, "edges_from_host_ms": ms_edges_h2d}
 
 
+def _timed_events(fn, reps):
+    """Mean ms of fn() over reps runs on the current stream (HIP events)."""
+    import torch
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def callers_side(dev, b, v, h, reps=10):
+    """Side measurement: the btb front-end (embedding
+    lookups + dropout, fwd+bwd) and both output heads (logits GEMM, softmax,
+    cross-entropy, dW/db/dX) at the bench's b, v, h.  The reference's
+    80+50+100+80 = 310-wide concat does not fit hidden 256, so the
+    tables are 64/32/96/64 wide here; heads o = 150 (output_size) and 46
+    (output_size_edges of the WSJ std->nivre lists)."""
+    import torch
+    from ggnn_amd.heads import EmbeddingFrontEnd, OutputHeads
+    rng = np.random.default_rng(11)
+    mk = lambda *s: torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32)).to(dev)
+    loc, pos, word = mk(150, 64), mk(46, 32), mk(40000, 96)
+    segs = [(loc, 0), (pos, 1), (word, 2), (loc, 3)]
+    wi = torch.from_numpy(np.stack([rng.integers(0, 150, (b, v)), rng.integers(0, 46, (b, v)),
+                                    rng.integers(0, 40000, (b, v)), rng.integers(0, 150, (b, v))],
+                                   2).astype(np.int32)).to(dev)
+    fe, oh = EmbeddingFrontEnd(h), OutputHeads(h)
+    heads = [(mk(2 * h, 150), mk(150)), (mk(2 * h, 46), mk(46))]
+    labels = []
+    for o in (150, 46):
+        y = np.zeros((b, v, o), np.float32)
+        y[np.arange(b)[:, None], np.arange(v)[None, :], rng.integers(0, o, (b, v))] = 1
+        labels.append(torch.from_numpy(y).to(dev))
+    hT, h0 = mk(b, v, h), mk(b, v, h)
+    dh0 = mk(b, v, h)
+    shared = torch.empty_like(loc)
+    dt = [shared, torch.empty_like(pos), torch.empty_like(word), shared]
+    state = {}
+
+    def heads_fb():
+        probs, _ = oh.forward(hT, h0, heads, labels, 0.85, 3, float(b))
+        oh.backward(hT, h0, heads, labels, probs, float(b))
+
+    ms_embed = _timed_events(lambda: (fe.forward(segs, wi, 0.55, 5), fe.backward(segs, wi, dh0, 0.55, 5, dtables=dt)),
+                             reps)
+    ms_heads = _timed_events(heads_fb, reps)
+    flops = 3 * 2 * b * v * 2 * h * (150 + 46)      # logits, dX, dW GEMMs
+    return {"embed_fwd_bwd_ms": ms_embed, "heads_fwd_bwd_ms": ms_heads,
+            "heads_gemm_tflops": flops / (ms_heads * 1e-3) / 1e12, "heads_peak_fp32_vector_tflops": 157.3,
+            "note": "fp32 FMA tiles (parity mode of the callers); tables 64/32/96/64 wide, heads o=150 and 46"}
+
+
+def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10):
+    """The same fwd+bwd step in a reduced-precision mode (single 16-bit MFMA
+    operands): graphs/s and the prop kernels' fraction of the dense bf16 MFMA
+    peak (north_star's >= 30 % target is quoted on bf16 tiles)."""
+    import torch
+    from ggnn_amd import _lib
+    from ggnn_amd.dist import FlatGradients
+    from ggnn_amd.engine import PropagationEngine
+    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=precision)
+    grads = FlatGradients(h, C, True, device=dev)
+    gv = dict(grads.views)
+    gv["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+    out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+
+    def step():
+        pack = eng.pack_weights(w_d, T=T)
+        eng.set_adjacency(A_d)
+        eng.forward(h0_d, pack, T, training=True, out=out)
+        eng.backward(dhT, gv)
+
+    ms = _timed_events(step, steps)
+    timer = _lib.KernelTimer(max_launches=200 * steps)
+    with timer:
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+    fr = {}
+    for k in ("prop_fwd", "prop_bwd", "gru_fwd", "gru_bwd", "wgrad"):
+        if timer.launches.get(k):
+            avg = timer.total_ms[k] / timer.launches[k]
+            fl = kernel_algo_flops(k, b, v, h, C, T)
+            fr[k] = {"avg_launch_ms": avg, "tflops": fl / (avg * 1e-3) / 1e12,
+                     "frac_of_bf16_peak": fl / (avg * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+    return {"precision": precision, "value": b / (ms * 1e-3), "unit": "graphs/s", "ms_per_step": ms,
+            "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
+
+
 def load_traffic():
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -146,6 +239,8 @@ def main():
     ap.add_argument("--dropout-keep", type=float, default=0.9,
                     help="keep probability of the dropout-on line (graph_state_dropout_keep_prob)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the side measurements (front-end/heads, bf16 mode)")
     ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (default nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -258,6 +353,9 @@ def main():
                  for k in kinds}
 
     feed_cmp = adjacency_feed_costs(eng, b, v, CFG["e"], dev) if rank == 0 else None
+    callers = callers_side(dev, b, v, h) if rank == 0 and not args.no_side else None
+    bf16 = (precision_side(dev, "bf16", A_d, h0_d, w_d, dhT, b, v, h, C, T)
+            if rank == 0 and not args.no_side and args.precision != "bf16" else None)
 
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]
@@ -290,6 +388,8 @@ def main():
                            "value": world * b / dt_drop, "ms_per_step": dt_drop * 1e3,
                            "note": "same step with the reference's training-feed dropout (:860-861); "
                                    "value above is dropout off (keep 1, the parity setting)"},
+            "callers": callers,
+            "bf16_mode": bf16,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

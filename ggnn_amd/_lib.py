@@ -23,9 +23,10 @@ EXPORTED = (
     "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
     "ggnn_set_adjacency_edges",
     "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
-    "ggnn_profile_end",
+    "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_heads_workspace_bytes",
+    "ggnn_heads_forward", "ggnn_heads_backward",
 )
-NUM_KERNEL_KINDS = 9
+NUM_KERNEL_KINDS = 10
 
 
 class GGNNDims(ctypes.Structure):
@@ -88,6 +89,17 @@ def load(path: str | None = None) -> ctypes.CDLL:
                                        ctypes.c_float, ctypes.c_int64, ctypes.c_float, _P, _P]
         lib.ggnn_dropout_mask.restype = _I
         lib.ggnn_dropout_mask.argtypes = [_DP, _I, _I, _P, _P]
+        U64, F = ctypes.c_uint64, ctypes.c_float
+        lib.ggnn_embed_forward.restype = _I
+        lib.ggnn_embed_forward.argtypes = [_DP, _P, _I, _P, _I, F, U64, _P, _P]
+        lib.ggnn_embed_backward.restype = _I
+        lib.ggnn_embed_backward.argtypes = [_DP, _P, _I, _P, _I, F, U64, _P, _P, _P, _P]
+        lib.ggnn_heads_workspace_bytes.restype = _I
+        lib.ggnn_heads_workspace_bytes.argtypes = [_DP, _P, _I, ctypes.POINTER(ctypes.c_size_t)]
+        lib.ggnn_heads_forward.restype = _I
+        lib.ggnn_heads_forward.argtypes = [_DP, _P, _I, _P, _P, F, U64, F, _P, _P, _P]
+        lib.ggnn_heads_backward.restype = _I
+        lib.ggnn_heads_backward.argtypes = [_DP, _P, _I, _P, _P, F, _P, _P, _P, _P, _P]
         lib.ggnn_kernel_kind_name.restype = ctypes.c_char_p
         lib.ggnn_kernel_kind_name.argtypes = [_I]
         lib.ggnn_profile_begin.restype = _I

@@ -17,6 +17,7 @@
 #include "k_prop.h"
 #include "k_optim.h"
 #include "k_wgrad.h"
+#include "k_head.h"
 
 // ---------------------------------------------------------------------------
 // error handling (thread-local last error; no exception crosses the ABI)
@@ -41,8 +42,9 @@ namespace {
 
 // ---- optional per-kernel-kind timing with HIP events (bench.py roofline)
 const char* const kKindNames[GGNN_NUM_KERNEL_KINDS] = {
-    "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad", "optimizer"};
-enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD, K_OPT };
+    "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad", "optimizer",
+    "heads"};
+enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD, K_OPT, K_HEADS };
 struct ProfState {
   bool on = false;
   int cap = 0, used = 0;
@@ -513,7 +515,7 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
 // ===========================================================================
 extern "C" {
 
-int ggnn_version(void) { return 3; }
+int ggnn_version(void) { return 4; }
 const char* ggnn_last_error(void) { return g_err.c_str(); }
 
 const char* ggnn_kernel_kind_name(int kind) {
@@ -671,7 +673,7 @@ int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_ra
   for (int i = 0; i < count; ++i) {
     const ggnn_adam_tensor& t = tensors[i];
     if (!t.param || !t.grad || !t.m || !t.v || t.n < 1) return fail(GGNN_EINVAL, "adam_step: bad tensor entry");
-    a.t[i] = OptTensor{t.param, t.grad, t.m, t.v, (long)t.n};
+    a.t[i] = OptTensor{t.param, t.grad, t.m, t.v, (long)t.n, t.sqnorm};
     a.begin[i] = off;
     off += t.n;
   }
@@ -784,6 +786,173 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
     case PREC_F16: return backward_impl<PREC_F16>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
     default: return backward_impl<PREC_BF16>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
   }
+}
+
+// ---- embedding front-end and output heads (k_head.h)
+static int plain_dims(const ggnn_dims* d, const char* what) {
+  if (!d) return fail(GGNN_EINVAL, std::string(what) + ": dims is NULL");
+  if (d->b < 1 || d->v < 1 || d->h < 1) return fail(GGNN_EINVAL, std::string(what) + ": b, v, h must be >= 1");
+  return GGNN_OK;
+}
+static int check_keep(float keep, const char* what) {
+  if (!(keep > 0.f && keep <= 1.f)) return fail(GGNN_EINVAL, std::string(what) + ": keep must lie in (0, 1]");
+  return GGNN_OK;
+}
+static int emb_args(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, int ncols, float keep, uint64_t seed,
+                    EmbArgs* a, const char* what) {
+  if (int e = plain_dims(d, what)) return e;
+  if (int e = check_keep(keep, what)) return e;
+  if (!segs || nseg < 1 || nseg > GGNN_EMBED_MAX_SEGMENTS)
+    return fail(GGNN_EINVAL, std::string(what) + ": 1.." + std::to_string(GGNN_EMBED_MAX_SEGMENTS) + " segments");
+  memset(a, 0, sizeof(*a));
+  int off = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const ggnn_embed_segment& g = segs[i];
+    if (!g.table || g.rows < 1 || g.width < 1 || g.column < 0 || g.column >= ncols)
+      return fail(GGNN_EINVAL, std::string(what) + ": bad segment " + std::to_string(i));
+    a->s[i] = EmbSeg{g.table, (long)g.rows, g.width, g.column, off};
+    off += g.width;
+  }
+  // the reference pads the concat up to hidden_size with tf.pad, which fails
+  // for a negative pad (80+50+100+80 = 310 > 256)
+  if (off > d->h)
+    return fail(GGNN_EINVAL, std::string(what) + ": embedding widths sum to " + std::to_string(off) + " > hidden " +
+                                 std::to_string(d->h) + " (negative pad)");
+  a->nseg = nseg;
+  a->ncols = ncols;
+  a->H = d->h;
+  a->rows = (long)d->b * d->v;
+  a->dr = make_drop(keep, seed);
+  return GGNN_OK;
+}
+
+int ggnn_embed_forward(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, const int32_t* word_inputs,
+                       int ncols, float keep, uint64_t seed, float* h0, ggnn_stream_t stream) {
+  EmbArgs a;
+  if (int e = emb_args(d, segs, nseg, ncols, keep, seed, &a, "embed_forward")) return e;
+  if (!word_inputs || !h0) return fail(GGNN_EINVAL, "embed_forward: NULL pointer");
+  hipStream_t s = (hipStream_t)stream;
+  Prof p(K_HEADS, s);
+  hipLaunchKernelGGL(k_embed_fwd, dim3(grid1d(a.rows * a.H)), dim3(256), 0, s, a, word_inputs, h0);
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, const int32_t* word_inputs,
+                        int ncols, float keep, uint64_t seed, const float* dh0, const float* dh0_add,
+                        float* lookup_sqnorm, ggnn_stream_t stream) {
+  EmbArgs a;
+  if (int e = emb_args(d, segs, nseg, ncols, keep, seed, &a, "embed_backward")) return e;
+  if (!word_inputs || !dh0 || !lookup_sqnorm) return fail(GGNN_EINVAL, "embed_backward: NULL pointer");
+  EmbGrad gd;
+  memset(&gd, 0, sizeof(gd));
+  hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < nseg; ++i) {
+    if (!segs[i].d_table) return fail(GGNN_EINVAL, "embed_backward: NULL d_table");
+    gd.dtable[i] = segs[i].d_table;
+    HIPCHK(hipMemsetAsync(segs[i].d_table, 0, (size_t)segs[i].rows * segs[i].width * 4, s));
+  }
+  HIPCHK(hipMemsetAsync(lookup_sqnorm, 0, (size_t)nseg * 4, s));
+  Prof p(K_HEADS, s);
+  hipLaunchKernelGGL(k_embed_bwd, dim3(std::min(grid1d(a.rows * a.H), 4096)), dim3(256), 0, s, a, gd, word_inputs,
+                     dh0, dh0_add, lookup_sqnorm);
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+namespace {
+struct HeadL {
+  size_t Wd[GGNN_MAX_HEADS], S[GGNN_MAX_HEADS], dZ[GGNN_MAX_HEADS], total;
+};
+int head_layout(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, HeadL* L, const char* what) {
+  if (int e = plain_dims(d, what)) return e;
+  if (!heads || nheads < 1 || nheads > GGNN_MAX_HEADS)
+    return fail(GGNN_EINVAL, std::string(what) + ": 1.." + std::to_string(GGNN_MAX_HEADS) + " heads");
+  const size_t rows = (size_t)d->b * d->v, K = 2 * (size_t)d->h;
+  size_t o = 0;
+  for (int i = 0; i < nheads; ++i) {
+    if (heads[i].o < 1 || !heads[i].weight || !heads[i].bias)
+      return fail(GGNN_EINVAL, std::string(what) + ": bad head " + std::to_string(i));
+    const size_t w = (size_t)heads[i].o;
+    L->Wd[i] = o; o += al(K * w * 4);
+    L->S[i] = o;  o += al(K * w * 4);
+    L->dZ[i] = o; o += al(rows * w * 4);
+  }
+  L->total = o;
+  return GGNN_OK;
+}
+}  // namespace
+
+int ggnn_heads_workspace_bytes(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, size_t* bytes) {
+  HeadL L;
+  if (int e = head_layout(d, heads, nheads, &L, "heads_workspace_bytes")) return e;
+  if (!bytes) return fail(GGNN_EINVAL, "heads_workspace_bytes: NULL pointer");
+  *bytes = L.total;
+  return GGNN_OK;
+}
+
+int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
+                       float keep, uint64_t seed, float target_num, float* loss, void* ws, ggnn_stream_t stream) {
+  HeadL L;
+  if (int e = head_layout(d, heads, nheads, &L, "heads_forward")) return e;
+  if (int e = check_keep(keep, "heads_forward")) return e;
+  if (!hT || !h0 || !ws) return fail(GGNN_EINVAL, "heads_forward: NULL pointer");
+  if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_forward: target_num must be > 0");
+  hipStream_t s = (hipStream_t)stream;
+  const int H = d->h, K = 2 * H;
+  const long rows = (long)d->b * d->v;
+  const Drop dr = make_drop(keep, seed);
+  if (loss) HIPCHK(hipMemsetAsync(loss, 0, (size_t)nheads * 4, s));
+  Prof p(K_HEADS, s);
+  for (int i = 0; i < nheads; ++i) {
+    const ggnn_output_head& hd = heads[i];
+    if (!hd.probs) return fail(GGNN_EINVAL, "heads_forward: NULL probs");
+    const int o = hd.o;
+    float* Wd = P<float>(ws, L.Wd[i]);
+    float* S = P<float>(ws, L.S[i]);
+    hipLaunchKernelGGL(k_head_wdrop, dim3(grid1d((long)K * o)), dim3(256), 0, s, hd.weight, K, o, i, dr, Wd, S);
+    HeadLogitsP q{hT, h0, Wd, hd.bias, hd.probs, (int)rows, o, K, H};
+    hipLaunchKernelGGL(k_sgemm<HeadLogitsP>, dim3((o + 63) / 64, (unsigned)((rows + 63) / 64), 1), dim3(256), 0, s, q);
+    hipLaunchKernelGGL(k_head_softmax, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, hd.probs,
+                       loss ? hd.labels : (const float*)nullptr, rows, o, 1.0f / target_num, loss ? loss + i : nullptr);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
+                        float target_num, const float* d_loss, void* ws, float* dhT, float* dh0,
+                        ggnn_stream_t stream) {
+  HeadL L;
+  if (int e = head_layout(d, heads, nheads, &L, "heads_backward")) return e;
+  if (!hT || !h0 || !ws || !dhT || !dh0) return fail(GGNN_EINVAL, "heads_backward: NULL pointer");
+  if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_backward: target_num must be > 0");
+  hipStream_t s = (hipStream_t)stream;
+  const int H = d->h, K = 2 * H;
+  const long rows = (long)d->b * d->v;
+  for (int i = 0; i < nheads; ++i)
+    if (!heads[i].labels || !heads[i].probs || !heads[i].d_weight || !heads[i].d_bias)
+      return fail(GGNN_EINVAL, "heads_backward: head needs labels, probs, d_weight, d_bias");
+  Prof p(K_HEADS, s);
+  for (int i = 0; i < nheads; ++i) {
+    const ggnn_output_head& hd = heads[i];
+    const int o = hd.o;
+    float* dZ = P<float>(ws, L.dZ[i]);
+    hipLaunchKernelGGL(k_head_dz, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, hd.probs, hd.labels, rows, o,
+                       1.0f / target_num, d_loss, dZ);
+    HeadDxP q{dZ, P<const float>(ws, L.Wd[i]), dhT, dh0, (int)rows, K, o, H, i > 0};
+    hipLaunchKernelGGL(k_sgemm<HeadDxP>, dim3(K / 64 + (K % 64 != 0), (unsigned)((rows + 63) / 64), 1), dim3(256), 0, s,
+                       q);
+    HIPCHK(hipMemsetAsync(hd.d_weight, 0, (size_t)K * o * 4, s));
+    HIPCHK(hipMemsetAsync(hd.d_bias, 0, (size_t)o * 4, s));
+    HeadDwP w{hT, h0, dZ, P<const float>(ws, L.S[i]), hd.d_weight, K, o, H, rows};
+    const unsigned splits = (unsigned)std::max<long>(1, std::min<long>(64, rows / 256));
+    hipLaunchKernelGGL(k_sgemm<HeadDwP>, dim3((o + 63) / 64, (K + 63) / 64, splits), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(k_colsum, dim3((o + 63) / 64, (unsigned)std::min<long>(256, rows)), dim3(64), 0, s, dZ, rows, o,
+                       hd.d_bias);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
 }
 
 }  // extern "C"

@@ -16,6 +16,7 @@ struct OptTensor {
   float* m;
   float* v;
   long n;
+  const float* sqo;  // squared-norm override (IndexedSlices norm), or nullptr
 };
 struct OptArgs {
   OptTensor t[GGNN_OPT_MAXT];
@@ -30,9 +31,11 @@ __global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict
   __shared__ float red[4];
   const OptTensor& T = a.t[blockIdx.y];
   float acc = 0.f;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < T.n; e += (long)gridDim.x * blockDim.x) {
-    const float g = a.gscale * T.g[e];
-    acc += g * g;
+  if (!T.sqo) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < T.n; e += (long)gridDim.x * blockDim.x) {
+      const float g = a.gscale * T.g[e];
+      acc += g * g;
+    }
   }
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -48,7 +51,7 @@ __global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __rest
     float x = 0.f;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += 64) x += sq[blockIdx.y * gridDim.x + i];
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
-    if (threadIdx.x == 0) tot = x;
+    if (threadIdx.x == 0) tot = T.sqo ? a.gscale * a.gscale * *T.sqo : x;
   }
   __syncthreads();
   // tf.clip_by_norm: t * clip / max(l2norm, clip)

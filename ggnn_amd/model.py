@@ -15,6 +15,11 @@ chem_tensorflow.py:70-136) that the hot path reads, with the same names:
   fixed_ts=None)`` -> [b, v, h] (:312-340), differentiable: its backward is the
   engine's HIP backward (the reference's TF autodiff, chem_tensorflow.py:496)
 * ``process_raw_graphs`` / ``make_minibatch_iterator`` (``BtbBatching``)
+* the callers either side of the path:
+  ``get_initial_node_representation`` (embedding front-end, :264-306),
+  ``gated_regression`` + the btb loss (:439-516, chem_tensorflow.py:326-421)
+  via ``build_loss()``, and ``train_step()`` (loss -> backward -> clip + Adam,
+  chem_tensorflow.py:483-506) -- all on the HIP library (``heads.py``).
 
 The arithmetic runs in libggnn.so; torch tensors only hold device memory and
 carry the autograd graph around the call.
@@ -26,8 +31,15 @@ import torch
 
 from .batching import BtbBatching
 from .engine import PropagationEngine
+from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
+from .optim import ClipAdam
 
 GRU_KEYS = ("gates_kernel", "gates_bias", "candidate_kernel", "candidate_bias")
+
+
+def mlp_init(shape, rng):
+    """utils.py MLP.init_weights: sqrt(6/(in+out)) * (2*rand - 1)."""
+    return (np.sqrt(6.0 / (shape[-2] + shape[-1])) * (2 * rng.rand(*shape).astype(np.float32) - 1)).astype(np.float32)
 
 
 def glorot_init(shape, rng=None):
@@ -74,7 +86,8 @@ class DenseGGNNChemModel(BtbBatching):
     """Hot-path subset of the reference's DenseGGNNChemModel (btb task)."""
 
     def __init__(self, args=None, params=None, num_edge_types=None, output_size_edges=12, pos_size=46,
-                 bucket_max_nodes=120, device=None, seed=None, precision="bf16"):
+                 bucket_max_nodes=120, device=None, seed=None, precision="bf16", vocab_size=1000, max_nodes=None,
+                 embedding_sizes=None):
         self.args = dict(args or {"--pr": "btb"})
         self.params = self.default_params()
         if params:
@@ -86,6 +99,16 @@ class DenseGGNNChemModel(BtbBatching):
         self.output_size_edges = int(output_size_edges)
         self.pos_size = int(pos_size)
         self.bucket_max_nodes = int(bucket_max_nodes)
+        # front-end sizes (chem_tensorflow.py:184-189; vocab/max_nodes come from
+        # the treebank lists there).  The reference's concat is 80+50+100+80 =
+        # 310 wide, so hidden_size < 310 needs smaller embeddings:
+        # embedding_sizes = dict(loc=, pos=, word=, edge=)
+        es = dict(loc=80, pos=50, word=100, edge=50)
+        es.update(embedding_sizes or {})
+        self.loc_embedding_size, self.pos_embedding_size = int(es["loc"]), int(es["pos"])
+        self.word_embedding_size, self.edge_embedding_size = int(es["word"]), int(es["edge"])
+        self.vocab_size = int(vocab_size)
+        self.max_nodes = int(max_nodes if max_nodes is not None else self.bucket_max_nodes)
         self.precision = precision
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.placeholders = {}
@@ -131,12 +154,47 @@ class DenseGGNNChemModel(BtbBatching):
             "candidate_kernel": t(glorot_init([2 * h, h], self._rng)),
             "candidate_bias": t(np.zeros([h], np.float32)),
         }
+        # front-end tables (chem_tensorflow_dense.py:214-235; tf.get_variable's
+        # default initializer is glorot-uniform)
+        self.weights["loc_embeddings"] = t(glorot_init([self.max_nodes, self.loc_embedding_size], self._rng))
+        self.weights["head_loc_embeddings"] = t(glorot_init([self.max_nodes, self.loc_embedding_size], self._rng))
+        self.weights["pos_embeddings"] = t(glorot_init([self.pos_size, self.pos_embedding_size], self._rng))
+        self.weights["word_embeddings"] = t(glorot_init([self.vocab_size, self.word_embedding_size], self._rng))
+        self.weights["edge_embeddings"] = t(glorot_init([self.num_edge_types + 1, self.edge_embedding_size],
+                                                        self._rng))
+        # out layers (chem_tensorflow.py:332-341): MLP(in, out, []) = one W, b;
+        # the regression_transform MLPs are built but unused by btb (:466)
+        o, oe = self.params["output_size"], self.output_size_edges
+        for task_id in self.params["task_ids"]:
+            for name, shape in (("regression_gate_task%i", [2 * h, o]), ("regression_gate_task_edges%i", [2 * h, oe]),
+                                ("regression_transform_task%i", [h, o]),
+                                ("regression_transform_task_edges%i", [h, oe])):
+                self.weights[name % task_id] = {"weights": [t(mlp_init(shape, self._rng))],
+                                                "biases": [t(np.zeros([shape[1]], np.float32))]}
+        self._front_end = None
+        self._heads = None
+        self.lookup_sqnorm = {}
+        self.optimizer = None
 
     def parameters(self):
         ps = [self.weights["edge_weights"], self.weights["edge_weights_fixed"]]
         if self.params["use_edge_bias"]:
             ps += [self.weights["edge_biases"], self.weights["edge_biases_fixed"]]
         ps += [self.weights["node_gru"][k] for k in GRU_KEYS]
+        return ps
+
+    def trainable_variables(self):
+        """The variables the btb loss reaches (TF passes None gradients for the
+        rest: the *_fixed twins, head_loc/edge embeddings, regression_transform)."""
+        ps = [self.weights["edge_weights"]]
+        if self.params["use_edge_bias"]:
+            ps.append(self.weights["edge_biases"])
+        ps += [self.weights["node_gru"][k] for k in GRU_KEYS]
+        ps += [self.weights[k] for k in ("loc_embeddings", "pos_embeddings", "word_embeddings")]
+        for task_id in self.params["task_ids"]:
+            for name in ("regression_gate_task%i", "regression_gate_task_edges%i"):
+                mlp = self.weights[name % task_id]
+                ps += [mlp["weights"][0], mlp["biases"][0]]
         return ps
 
     # -------------------------------------------------------------- feeds
@@ -210,3 +268,84 @@ class DenseGGNNChemModel(BtbBatching):
         self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=seed)
         self.ops["final_node_representations" if fixed_ts is None else "second_node_representations"] = out
         return out
+
+    # ------------------------------------------------- §8f rank 1: callers
+    def get_initial_node_representation(self):
+        """btb front-end (chem_tensorflow_dense.py:264-306): lookups of
+        word_inputs columns 0 (loc), 1 (pos), 2 (word), 3 (head loc, the loc
+        table again), each dropped out with emb_dropout_keep_prob, concatenated
+        and zero-padded to hidden_size.  Columns 4, 5 (head POS, edge) are
+        looked up by the reference but unused; they are not gathered here."""
+        if "word_inputs" not in self.placeholders:
+            raise RuntimeError("feed() a minibatch with word_inputs first")
+        h = self.params["hidden_size"]
+        width = self.loc_embedding_size * 2 + self.pos_embedding_size + self.word_embedding_size
+        if width > h:
+            raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
+                             "(SURVEY F7); pass smaller embedding_sizes" % (width, h))
+        W = self.weights
+        tables = (W["loc_embeddings"], W["pos_embeddings"], W["word_embeddings"], W["loc_embeddings"])
+        cols = (0, 1, 2, 3)
+        wi = word_inputs_tensor(self.placeholders["word_inputs"], self.device,
+                                {c: tb.shape[0] for tb, c in zip(tables, cols)})
+        keep = float(self.placeholders.get("emb_dropout_keep_prob", 1.0))
+        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        if self._front_end is None:
+            self._front_end = EmbeddingFrontEnd(h)
+        h0 = EmbedFunction.apply(self._front_end, self, wi, keep, seed, cols, *tables)
+        self.last_embed = dict(keep=keep, seed=seed)
+        self.ops["initial_node_representations"] = h0
+        return h0
+
+    def build_loss(self, task_id=0):
+        """make_model for btb (chem_tensorflow.py:326-421): h0 -> h_T -> both
+        gated_regression heads on [h_T, h0] -> loss = heads CE + edges CE, each
+        over task_target_num = sum(target_mask[task]) + SMALL_NUMBER."""
+        h0 = self.get_initial_node_representation()
+        hT = self.compute_final_node_representations(h0)
+        b, v, h = hT.shape
+        o, oe = self.params["output_size"], self.output_size_edges
+        if v > o:
+            raise ValueError("num_vertices %d > output_size %d" % (v, o))
+        y_h = torch.from_numpy(np.asarray(self.placeholders["target_values_head"], np.float32).reshape(b, v, o))
+        y_e = torch.from_numpy(np.asarray(self.placeholders["target_values_edges"], np.float32).reshape(b, v, oe))
+        labels = [y_h.to(self.device), y_e.to(self.device)]
+        tmask = np.asarray(self.placeholders["target_mask"], np.float64)
+        internal = self.params["task_ids"].index(task_id)
+        target_num = float(tmask[internal].sum() + SMALL_NUMBER)
+        keep = float(self.placeholders.get("out_layer_dropout_keep_prob",
+                                           self.params["out_layer_dropout_keep_prob"]))
+        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        if self._heads is None:
+            self._heads = OutputHeads(h)
+        g = self.weights["regression_gate_task%i" % task_id]
+        ge = self.weights["regression_gate_task_edges%i" % task_id]
+        loss, probs, probs_e = HeadsFunction.apply(self._heads, labels, keep, seed, target_num, hT, h0,
+                                                   g["weights"][0], g["biases"][0], ge["weights"][0], ge["biases"][0])
+        self.ops["loss"] = loss
+        self.ops["computed_values"] = probs.reshape(b, v * o)
+        self.ops["computed_values_edges"] = probs_e.reshape(b, v * oe)
+        self.last_heads = dict(keep=keep, seed=seed, target_num=target_num)
+        return loss
+
+    def train_step(self, feed_dict=None, grad_scale=1.0, all_reduce=None):
+        """One training step (chem_tensorflow.py:483-506 + run_epoch's
+        sess.run of train_step): loss, backward, per-variable clip_by_norm,
+        Adam.  all_reduce: optional callable on the list of gradients (data
+        parallel; pass grad_scale = 1/N).  Returns the loss tensor."""
+        if feed_dict is not None:
+            self.feed(feed_dict)
+        params = self.trainable_variables()
+        for p in params:
+            p.grad = None
+        loss = self.build_loss()
+        loss.backward()
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+        if all_reduce is not None:
+            all_reduce(grads)
+        if self.optimizer is None:
+            self.optimizer = ClipAdam(params, learning_rate=self.params["learning_rate"],
+                                      clamp_gradient_norm=self.params["clamp_gradient_norm"])
+        sq = [self.lookup_sqnorm.get(id(p)) for p in params]
+        self.optimizer.step(grads, grad_scale=grad_scale, sqnorms=sq)
+        return loss

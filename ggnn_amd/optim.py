@@ -17,7 +17,7 @@ from . import _lib
 
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("m", ctypes.c_void_p),
-                ("v", ctypes.c_void_p), ("n", ctypes.c_int64)]
+                ("v", ctypes.c_void_p), ("n", ctypes.c_int64), ("sqnorm", ctypes.c_void_p)]
 
 
 MAX_TENSORS = 16
@@ -50,15 +50,21 @@ class ClipAdam:
         self._lib = _lib.load()
 
     @torch.no_grad()
-    def step(self, grads, grad_scale: float = 1.0) -> None:
+    def step(self, grads, grad_scale: float = 1.0, sqnorms=None) -> None:
+        """sqnorms: optional list (None entries allowed) of device scalars that
+        replace ||grad||^2 in clip_by_norm -- the per-lookup norm of an
+        embedding's IndexedSlices gradient (EmbeddingFrontEnd.backward)."""
         grads = list(grads)
+        sqnorms = list(sqnorms) if sqnorms is not None else [None] * len(grads)
         if len(grads) != len(self.params):
             raise ValueError("expected %d gradients, got %d" % (len(self.params), len(grads)))
         tab = (AdamTensor * len(self.params))()
         for i, (p, g) in enumerate(zip(self.params, grads)):
             if g.shape != p.shape or g.dtype != torch.float32 or not g.is_contiguous():
                 raise ValueError("gradient %d must be contiguous fp32 of shape %s" % (i, tuple(p.shape)))
-            tab[i] = AdamTensor(p.data_ptr(), g.data_ptr(), self.m[i].data_ptr(), self.v[i].data_ptr(), p.numel())
+            sq = sqnorms[i]
+            tab[i] = AdamTensor(p.data_ptr(), g.data_ptr(), self.m[i].data_ptr(), self.v[i].data_ptr(), p.numel(),
+                                None if sq is None else sq.data_ptr())
         self.t += 1
         _lib.check(self._lib.ggnn_adam_step(tab, len(self.params), self.lr, self.b1, self.b2, self.eps, self.clip,
                                             self.t, float(grad_scale), ctypes.c_void_p(self._scratch.data_ptr()),

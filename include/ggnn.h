@@ -168,6 +168,11 @@ typedef struct ggnn_adam_tensor {
   float* m;  /* first-moment slot, zero-initialised by the caller */
   float* v;  /* second-moment slot, zero-initialised by the caller */
   int64_t n;
+  /* NULL, or a device float holding the squared norm clip_by_norm must use
+   * instead of ||grad||^2 (before grad_scale): an embedding's gradient is an
+   * IndexedSlices in the reference, whose norm runs over the per-lookup rows
+   * (ggnn_embed_backward's lookup_sqnorm) */
+  const float* sqnorm;
 } ggnn_adam_tensor;
 #define GGNN_ADAM_MAX_TENSORS 16
 int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate,
@@ -179,10 +184,71 @@ int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_ra
  * ([C][h][h] bytes), kind 1 = state mask of timestep t ([b][v][h] bytes). */
 int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_stream_t stream);
 
+/* ---- The callers either side of the path (btb task) ----
+ *
+ * Embedding front-end: get_initial_node_representation,
+ * chem_tensorflow_dense.py:264-306.  Segment s copies row
+ * word_inputs[g][i][column_s] of table_s into columns [o_s, o_s + width_s) of
+ * h0[g][i] (o_s = sum of the earlier widths), times an embedding-dropout mask /
+ * keep (tf.nn.dropout, keep = placeholders['emb_dropout_keep_prob']); columns
+ * past the last segment are zero (the tf.pad to hidden_size, :303-305).  The
+ * widths must sum to <= d->h (the reference's tf.pad fails otherwise).  Uses
+ * d->b, d->v, d->h.  Rows outside [0, rows) give zero vectors (validate on the
+ * host: tf.nn.embedding_lookup raises for them on the CPU). */
+typedef struct ggnn_embed_segment {
+  const float* table; /* [rows][width] fp32 */
+  float* d_table;     /* its gradient (ggnn_embed_backward; overwritten) */
+  int64_t rows;
+  int32_t width;
+  int32_t column;     /* column of word_inputs indexing this table */
+} ggnn_embed_segment;
+#define GGNN_EMBED_MAX_SEGMENTS 8
+int ggnn_embed_forward(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg,
+                       const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
+                       float* h0, ggnn_stream_t stream);
+/* Gradients of the tables from dL/dh0 (+ dh0_add when not NULL: the two uses
+ * of h0, the propagation input and the heads' concat), same keep and seed as
+ * the forward.  lookup_sqnorm: device float[nseg], per segment the sum of
+ * squares of its per-lookup gradient rows (overwritten). */
+int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg,
+                        const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
+                        const float* dh0, const float* dh0_add, float* lookup_sqnorm,
+                        ggnn_stream_t stream);
+
+/* Output heads: gated_regression for --pr btb, chem_tensorflow_dense.py:439-516
+ * with MLP(2h, o, [], out_layer_dropout_keep_prob) (utils.py:40-84), and the
+ * btb loss, chem_tensorflow.py:349-403:
+ *   z = [h_T | h0] @ (W * mask / keep) + b      (rows = b*v nodes)
+ *   probs = softmax(z) over o                    (computed_values [b, v*o])
+ *   loss  = sum_rows -sum_o labels * log(probs) / target_num
+ * target_num = sum(target_mask[task]) + SMALL_NUMBER (the caller's host
+ * value).  One mask per head per step (keep, seed). */
+typedef struct ggnn_output_head {
+  const float* weight; /* MLP_W_layer0 [2h][o] */
+  const float* bias;   /* MLP_b_layer0 [o] */
+  int32_t o;
+  const float* labels; /* [b][v][o] targets, or NULL (no loss) */
+  float* probs;        /* [b][v][o] out */
+  float* d_weight;     /* [2h][o] (backward; overwritten) */
+  float* d_bias;       /* [o]     (backward; overwritten) */
+} ggnn_output_head;
+#define GGNN_MAX_HEADS 4
+int ggnn_heads_workspace_bytes(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, size_t* bytes);
+/* loss: device float[nheads], overwritten (per head; the reference's loss is
+ * their sum).  ws is kept for ggnn_heads_backward. */
+int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                       const float* h0, float keep, uint64_t seed, float target_num, float* loss,
+                       void* ws, ggnn_stream_t stream);
+/* d_loss: device float (dL/dloss, e.g. 1) or NULL for 1.  dhT, dh0: [b][v][h],
+ * overwritten with the heads' contributions. */
+int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                        const float* h0, float target_num, const float* d_loss, void* ws, float* dhT,
+                        float* dh0, ggnn_stream_t stream);
+
 /* Optional per-kernel timing (HIP events around every launch of the library
  * on the launch's stream), used by bench.py for the roofline.  Not for use
  * under graph capture.  total_ms / launches: arrays of GGNN_NUM_KERNEL_KINDS. */
-#define GGNN_NUM_KERNEL_KINDS 9
+#define GGNN_NUM_KERNEL_KINDS 10
 const char* ggnn_kernel_kind_name(int kind);
 int ggnn_profile_begin(int max_launches);
 int ggnn_profile_end(double* total_ms, int* launches);

@@ -19,3 +19,12 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+@pytest.fixture(scope="session")
+def lib():
+    """libggnn.so, built in-tree if stale (host-side entry points only on CPU)."""
+    from ggnn_amd import build, _lib
+    if build.needs_build():
+        build.build()
+    return _lib.load()

@@ -1,0 +1,192 @@
+"""GPU parity of the callers either side of the path:
+embedding front-end, output heads + btb loss, and a whole btb training step
+of the drop-in model, each against the float64 oracle on the same inputs and
+the same Philox masks.  fp32 arithmetic: tolerance 1e-3 (north_star), the
+kernels land near 1e-6."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import ggnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-3
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a machine without a HIP device")
+    return torch
+
+
+def _nmax(x, ref):
+    return float(np.abs(np.asarray(x, np.float64) - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+@pytest.mark.parametrize("keep", [1.0, 0.55])
+def test_embed_forward_backward_parity(keep):
+    torch = _torch()
+    from ggnn_amd.heads import EmbeddingFrontEnd
+    rng = np.random.default_rng(3)
+    b, v, h = 5, 23, 64
+    loc = rng.normal(size=(30, 16)).astype(np.float32)
+    pos = rng.normal(size=(12, 8)).astype(np.float32)
+    word = rng.normal(size=(50, 24)).astype(np.float32)
+    wi = np.stack([rng.integers(0, 30, (b, v)), rng.integers(0, 12, (b, v)), rng.integers(0, 50, (b, v)),
+                   rng.integers(0, 30, (b, v)), rng.integers(0, 12, (b, v)), rng.integers(0, 5, (b, v))], axis=2)
+    segs_np = [(loc, 0), (pos, 1), (word, 2), (loc, 3)]
+    dev = torch.device("cuda")
+    T = {id(a): torch.from_numpy(a).to(dev) for a in (loc, pos, word)}
+    segs = [(T[id(a)], c) for a, c in segs_np]
+    wi_t = torch.from_numpy(wi.astype(np.int32)).to(dev)
+    fe = EmbeddingFrontEnd(h)
+    seed = 0xABCDEF12345
+    h0 = fe.forward(segs, wi_t, keep, seed)
+    ref = O.embed_forward(segs_np, wi, h, keep, seed)
+    assert np.abs(h0.cpu().numpy() - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+    G = rng.normal(size=(b, v, h)).astype(np.float32)
+    G2 = rng.normal(size=(b, v, h)).astype(np.float32)
+    shared = torch.empty_like(T[id(loc)])
+    dts, sq = fe.backward(segs, wi_t, torch.from_numpy(G).to(dev), keep, seed, dh0_add=torch.from_numpy(G2).to(dev),
+                          dtables=[shared, torch.empty_like(T[id(pos)]), torch.empty_like(T[id(word)]), shared])
+    rd, rsq = O.embed_backward(segs_np, wi, h, G.astype(np.float64) + G2, keep, seed)
+    assert _nmax(dts[0].cpu().numpy(), rd[0] + rd[3]) <= 1e-5
+    assert _nmax(dts[1].cpu().numpy(), rd[1]) <= 1e-5
+    assert _nmax(dts[2].cpu().numpy(), rd[2]) <= 1e-5
+    np.testing.assert_allclose(sq.cpu().numpy(), rsq, rtol=1e-5)
+
+
+@pytest.mark.parametrize("b,v,h,os_,keep", [(4, 20, 64, (150, 12), 1.0), (3, 37, 128, (150, 46), 0.85),
+                                            (2, 128, 256, (150, 46), 0.85)])
+def test_heads_forward_backward_parity(b, v, h, os_, keep):
+    torch = _torch()
+    from ggnn_amd.heads import OutputHeads
+    rng = np.random.default_rng(b * v)
+    dev = torch.device("cuda")
+    hT = rng.uniform(-1, 1, (b, v, h)).astype(np.float32)
+    h0 = rng.uniform(-0.5, 0.5, (b, v, h)).astype(np.float32)
+    heads_np, heads_t, labels = [], [], []
+    for o in os_:
+        W = (np.sqrt(6.0 / (2 * h + o)) * (2 * rng.random((2 * h, o)) - 1)).astype(np.float32)
+        bb = rng.normal(size=o).astype(np.float32) * 0.1
+        y = np.zeros((b, v, o), np.float32)
+        y[np.arange(b)[:, None], np.arange(v)[None, :], rng.integers(0, min(o, v), (b, v))] = 1
+        y[:, v - 3:] = 0                                    # padded nodes
+        heads_np.append(dict(W=W, b=bb, labels=y))
+        heads_t.append((torch.from_numpy(W).to(dev), torch.from_numpy(bb).to(dev)))
+        labels.append(torch.from_numpy(y).to(dev))
+    tn = float(b) + O.SMALL_NUMBER
+    seed = 99
+    oh = OutputHeads(h)
+    hT_t, h0_t = torch.from_numpy(hT).to(dev), torch.from_numpy(h0).to(dev)
+    probs, loss = oh.forward(hT_t, h0_t, heads_t, labels, keep, seed, tn)
+    rp, rl = O.heads_forward(hT, h0, heads_np, keep, seed, tn)
+    for i in range(len(os_)):
+        assert np.abs(probs[i].cpu().numpy() - rp[i]).max() <= 1e-5
+        assert abs(float(loss[i]) - rl[i]) <= 1e-5 * abs(rl[i]) + 1e-6
+    dws, dbs, dhT, dh0 = oh.backward(hT_t, h0_t, heads_t, labels, probs, tn)
+    rw, rb, rhT, rh0 = O.heads_backward(hT, h0, heads_np, [p.cpu().numpy() for p in probs], keep, seed, tn)
+    for i in range(len(os_)):
+        assert _nmax(dws[i].cpu().numpy(), rw[i]) <= 1e-5
+        assert _nmax(dbs[i].cpu().numpy(), rb[i]) <= 1e-5
+    assert _nmax(dhT.cpu().numpy(), rhT) <= 1e-5
+    assert _nmax(dh0.cpu().numpy(), rh0) <= 1e-5
+
+
+def _dev_model(torch, keep_all):
+    from ggnn_amd.model import DenseGGNNChemModel
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
+    data = json.loads(str(g["raw_json"]))
+    vocab = 1 + max(max(d["words_index"]) for d in data)
+    params = {"hidden_size": 128, "num_timesteps": 2, "batch_size": 6, "learning_rate": 0.003}
+    if keep_all:
+        params.update(graph_state_dropout_keep_prob=1.0, emb_dropout_keep_prob=1.0, out_layer_dropout_keep_prob=1.0)
+    m = DenseGGNNChemModel(params=params, num_edge_types=int(g["num_edge_types"]),
+                           output_size_edges=int(g["output_size_edges"]), pos_size=int(g["pos_size"]),
+                           bucket_max_nodes=int(g["bucket_max_nodes"]), precision="fp32", vocab_size=vocab,
+                           embedding_sizes=dict(loc=16, pos=8, word=16, edge=8))
+    feeds = list(m.make_minibatch_iterator(m.process_raw_graphs(data[:30], True), True))
+    return m, feeds
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_model_train_step_matches_oracle(dropout):
+    """One whole btb training step of the drop-in model on real dev batches
+    (front-end -> propagation -> heads -> loss -> backward -> clip + Adam)
+    against the oracle composed the same way, including the IndexedSlices
+    clip norm of the embeddings and every dropout mask (replayed from the
+    seeds the model drew)."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=not dropout)
+    fd = feeds[0]
+    if dropout:
+        fd = dict(fd, edge_weight_dropout_keep_prob=0.9, graph_state_keep_prob=0.9)
+    params = m.trainable_variables()
+    before = [p.detach().cpu().numpy().astype(np.float64) for p in params]
+    loss = m.train_step(fd)
+    after = [p.detach().cpu().numpy() for p in params]
+    # ---- oracle
+    W = m.weights
+    nm = {id(p): i for i, p in enumerate(params)}
+    P = lambda t: before[nm[id(t)]]
+    h = m.params["hidden_size"]
+    wi = np.asarray(fd["word_inputs"]).astype(np.int64)
+    segs = [(P(W["loc_embeddings"]), 0), (P(W["pos_embeddings"]), 1), (P(W["word_embeddings"]), 2),
+            (P(W["loc_embeddings"]), 3)]
+    e = m.last_embed
+    h0 = O.embed_forward(segs, wi, h, e["keep"], e["seed"])
+    w64 = {"edge_weights": P(W["edge_weights"]), "edge_biases": P(W["edge_biases"])}
+    w64.update({k: P(t) for k, t in W["node_gru"].items()})
+    A = np.asarray(fd["adjacency_matrix"], np.float64)
+    dr = m.last_dropout
+    hT, caches = O.forward(A, h0, w64, m.params["num_timesteps"],
+                           dropout=dict(edge_keep=dr["edge_keep"], state_keep=dr["state_keep"], seed=dr["seed"]))
+    b, v = fd["num_graphs"], fd["num_vertices"]
+    o, oe = m.params["output_size"], m.output_size_edges
+    g0, ge = W["regression_gate_task0"], W["regression_gate_task_edges0"]
+    heads = [dict(W=P(g0["weights"][0]), b=P(g0["biases"][0]),
+                  labels=np.asarray(fd["target_values_head"], np.float64).reshape(b, v, o)),
+             dict(W=P(ge["weights"][0]), b=P(ge["biases"][0]),
+                  labels=np.asarray(fd["target_values_edges"], np.float64).reshape(b, v, oe))]
+    hd = m.last_heads
+    probs, losses = O.heads_forward(hT, h0, heads, hd["keep"], hd["seed"], hd["target_num"])
+    assert abs(float(loss.detach()) - sum(losses)) <= TOL * abs(sum(losses))
+    dWs, dbs, dhT, dh0_heads = O.heads_backward(hT, h0, heads, probs, hd["keep"], hd["seed"], hd["target_num"])
+    gp = O.backward(A, dhT, caches, w64)
+    dts, sq = O.embed_backward(segs, wi, h, dh0_heads + gp["h0"], e["keep"], e["seed"])
+    grads = [gp["edge_weights"], gp["edge_biases"]] + [gp[k] for k in ("gates_kernel", "gates_bias", "candidate_kernel",
+                                                                      "candidate_bias")]
+    grads += [dts[0] + dts[3], dts[1], dts[2], dWs[0], dbs[0], dWs[1], dbs[1]]
+    sqn = [None] * 6 + [sq[0] + sq[3], sq[1], sq[2]] + [None] * 4
+    # TF1 Adam step 1 with clip_by_norm (IndexedSlices norm for the tables)
+    lr, clip = m.params["learning_rate"], m.params["clamp_gradient_norm"]
+    lr_t = lr * np.sqrt(1 - 0.999) / (1 - 0.9)
+    for i, (p0, g) in enumerate(zip(before, grads)):
+        assert _nmax(params[i].grad.cpu().numpy(), g) <= TOL, i
+        if sqn[i] is not None:
+            got = m.lookup_sqnorm[id(params[i])]
+            assert abs(float(got) - sqn[i]) <= 1e-4 * sqn[i], i
+        n = np.sqrt(sqn[i]) if sqn[i] is not None else np.sqrt(np.sum(g * g))
+        gc = g * clip / max(n, clip)
+        mm, vv = 0.1 * gc, 0.001 * gc * gc
+        ref = p0 - lr_t * mm / (np.sqrt(vv) + 1e-8)
+        # Adam's first step is ~lr * sign(g): compare it where the gradient is
+        # not at rounding level (there a 1e-6 error may flip the sign)
+        sig = np.abs(gc) > 1e-3 * max(np.abs(gc).max(), 1e-30)
+        assert np.abs(after[i] - ref)[sig].max(initial=0.0) <= lr * 1e-2, i
+        assert np.abs(after[i] - ref).max() <= 2.01 * lr, i
+
+
+def test_model_trains_on_dev_batches():
+    """Loss goes down over a few steps on real dev batches (sanity of the
+    whole btb training loop on the GPU)."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=True)
+    fd = feeds[0]
+    losses = [float(m.train_step(fd).detach()) for _ in range(8)]
+    assert np.isfinite(losses).all()
+    assert losses[-1] < 0.9 * losses[0]

@@ -8,14 +8,6 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.fixture(scope="module")
-def lib():
-    from ggnn_amd import build, _lib
-    if build.needs_build():
-        build.build()
-    return _lib.load()
-
-
 def declared_symbols():
     with open(os.path.join(ROOT, "include", "ggnn.h")) as f:
         src = f.read()
