@@ -13,6 +13,7 @@
 #include "../../include/ggnn.h"
 #include "ggnn_common.h"
 #include "k_gru.h"
+#include "k_gru2.h"
 #include "k_prep.h"
 #include "k_prop.h"
 #include "k_optim.h"
@@ -251,6 +252,15 @@ void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const fl
                     const void* pk, float* hf_out, u16* hb_out, void* hT, float* r, float* u, float* cc, void* rhT,
                     hipStream_t s) {
   Prof p(K_GRU_FWD, s);
+  if constexpr (Prec<PREC>::split && H == 256) {
+    // 128-row tiles with K-streamed activations (k_gru2.h)
+    if (c.N % 128 == 0) {
+      hipLaunchKernelGGL(k_gru_fwd2, dim3(c.N / 128), dim3(512), 0, s, (const float*)Xa, hf, P<u16>(pk, PL.Wg),
+                         P<float>(pk, PL.bg), P<u16>(pk, PL.Wc), P<float>(pk, PL.bc), PL.loWg, PL.loWc, hf_out,
+                         (u16*)hT, r, u, cc, (u16*)rhT, c.N, c.sdrop, t, c.vsh);
+      return;
+    }
+  }
   hipLaunchKernelGGL((k_gru_fwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, (const ActT<PREC>*)Xa, hb,
                      hf, P<u16>(pk, PL.Wg), P<float>(pk, PL.bg), P<u16>(pk, PL.Wc), P<float>(pk, PL.bc), PL.loWg,
                      PL.loWc, hf_out, hb_out, (u16*)hT, r, u, cc, (u16*)rhT, c.N, c.sdrop, t, c.vsh);
@@ -514,6 +524,9 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
 // C ABI
 // ===========================================================================
 extern "C" {
+#ifdef GGNN_TS
+int ggnn_dbg_ts(void* host) { return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ts), sizeof(g_ts)); }
+#endif
 
 int ggnn_version(void) { return 4; }
 const char* ggnn_last_error(void) { return g_err.c_str(); }

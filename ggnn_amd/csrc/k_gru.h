@@ -14,6 +14,7 @@
 // weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
 // full unrolling, which spills at H = 256)
 constexpr int GF_UNROLL = 2, GB_UNROLL = 2;
+
 // gru_bwd elementwise phases: loads of GB_GROUP row quads (x 4 arrays) in flight
 // between scheduling barriers (measured: 4 > 2 > 1; VGPRs stay within budget)
 constexpr int GB_GROUP = 4, GB_GROUP2 = 4;
@@ -46,11 +47,12 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   const int tid = threadIdx.x, lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int n = ns * 32 + l32;
   const long row0 = (long)blockIdx.x * R;
-
+  TSMARK(0, 0);
   stage_rows<PREC, R, H, NT>(x_hi, x_lo, Xa + row0 * H, H, tid);
   if constexpr (SPLIT) stage_rows<PREC_SPLIT, R, H, NT>(h_hi, h_lo, hf + row0 * H, H, tid);
   else stage_rows<PREC, R, H, NT>(h_hi, h_lo, hb16 + row0 * H, H, tid);
   __syncthreads();
+  TSMARK(0, 1);
 
   f32x16 ar[RT], au[RT];
   {
@@ -75,6 +77,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(au[rt], ah, al, w.c, w.d);
     }
   });
+  TSMARK(0, 2);
   const rsrc_t rh_in = mkrsrc(hf + row0 * H, R * H * 4);
   const int vo = (4 * hh * H + n) * 4;
 #pragma unroll
@@ -118,6 +121,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
     }
   }
   __syncthreads();
+  TSMARK(0, 3);
   // ---- pass B: candidate
   f32x16 ac[RT];
   {
@@ -139,6 +143,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       mma<PREC>(ac[rt], qh, ql, w.c, w.d);
     }
   });
+  TSMARK(0, 4);
   // ---- blend + outputs
   const rsrc_t ho = mkrsrc(hf_out + row0 * H, R * H * 4);
   uint4 dw = make_uint4(0, 0, 0, 0);
@@ -191,6 +196,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       st16(hb_out + (row0 + row) * H + ch * 8, ld16(h_hi + SH::off(row, ch)));
     }
   }
+  TSMARK(0, 5);
 }
 
 // ===========================================================================
@@ -227,6 +233,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
                pu = mkrsrc(uin + tb0, tbytes), pc = mkrsrc(cin + tb0, tbytes);
   const int vo = (4 * hh * H + n) * 4;
   const long twg = wg_off(n, row0 + 4 * hh, H);  // dX^T, dzc^T, dzg^T: K-blocked [H][N] arrays
+  TSMARK(1, 0);
 
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
@@ -259,6 +266,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   usum += __shfl_xor(usum, 32);
   if (hh == 0) { atomicAdd(dbc + n, csum); atomicAdd(dbg + H + n, usum); }
   __syncthreads();
+  TSMARK(1, 1);
 
   // ---- product 1: [dX1 | d(rh)] = dzc @ Wc^T
   f32x16 a1[RT], a2[RT];
@@ -278,6 +286,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     }
   });
   __syncthreads();  // dzc reads done
+  TSMARK(1, 2);
 
   // ---- phase 2: dh (into a2), the r half of dzg
   float rsum = 0.f;
@@ -305,6 +314,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   rsum += __shfl_xor(rsum, 32);
   if (hh == 0) atomicAdd(dbg + n, rsum);
   __syncthreads();
+  TSMARK(1, 3);
 
   // ---- product 2: [dX2 | dh2] = dzg @ Wg^T
   auto ld2 = [&](int ks) {
@@ -320,6 +330,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       mma<PREC>(a2[rt], ah, al, w.c, w.d);
     }
   });
+  TSMARK(1, 4);
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -330,4 +341,5 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
     for (int r = 0; r < 16; ++r) bst(pdo, a2[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
   }
+  TSMARK(1, 5);
 }
