@@ -48,6 +48,8 @@ def kernel_algo_flops(kind, b, v, h, C, T):
         return b * (f["mt"] + f["agg"])
     if kind in ("gru_fwd", "gru_bwd"):
         return b * f["gru"]
+    if kind == "fwd_fused":  # the whole T-step forward (messages + GRU) in one launch
+        return b * f["fwd"]
     if kind == "wgrad":   # dW (MT-sized) + dWg, dWc (GRU-sized) over all T steps
         return T * b * (f["mt"] + f["gru"])
     return 0
@@ -208,7 +210,7 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10)
             step()
         torch.cuda.synchronize()
     fr = {}
-    for k in ("prop_fwd", "prop_bwd", "gru_fwd", "gru_bwd", "wgrad"):
+    for k in ("fwd_fused", "prop_fwd", "prop_bwd", "gru_fwd", "gru_bwd", "wgrad"):
         if timer.launches.get(k):
             avg = timer.total_ms[k] / timer.launches[k]
             fl = kernel_algo_flops(k, b, v, h, C, T)

@@ -26,7 +26,7 @@ EXPORTED = (
     "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_heads_workspace_bytes",
     "ggnn_heads_forward", "ggnn_heads_backward",
 )
-NUM_KERNEL_KINDS = 10
+NUM_KERNEL_KINDS = 11
 
 
 class GGNNDims(ctypes.Structure):

@@ -14,6 +14,7 @@
 #include "ggnn_common.h"
 #include "k_gru.h"
 #include "k_gru2.h"
+#include "k_fused.h"
 #include "k_prep.h"
 #include "k_prop.h"
 #include "k_optim.h"
@@ -44,8 +45,8 @@ namespace {
 // ---- optional per-kernel-kind timing with HIP events (bench.py roofline)
 const char* const kKindNames[GGNN_NUM_KERNEL_KINDS] = {
     "pack_weights", "prep_adjacency", "state_io", "prop_fwd", "gru_fwd", "gru_bwd", "prop_bwd", "wgrad", "optimizer",
-    "heads"};
-enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD, K_OPT, K_HEADS };
+    "heads", "fwd_fused"};
+enum { K_PACK = 0, K_ADJ, K_IO, K_PROP_FWD, K_GRU_FWD, K_GRU_BWD, K_PROP_BWD, K_WGRAD, K_OPT, K_HEADS, K_FWD_FUSED };
 struct ProfState {
   bool on = false;
   int cap = 0, used = 0;
@@ -350,6 +351,45 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
                        dense ? (float*)nullptr : hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N,
                        (int)Prec<PREC>::f16, kNoDrop, 0);
   }
+  if (SPLIT && c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT) {
+    // the whole T-step forward of each graph in one workgroup (k_fused.h)
+    FusedFwdArgs fa;
+    memset(&fa, 0, sizeof(fa));
+    fa.Ab = P<u16>(adj, AL.Ab);
+    fa.Wp = P<u16>(pack, PL.wf(0));
+    fa.wlo = PL.loW;
+    fa.wstep = c.ed ? (long)(PL.szW / 2) : 0;
+    fa.beta = P<float>(pack, PL.beta);
+    fa.Wgp = P<u16>(pack, PL.Wg);
+    fa.bg = P<float>(pack, PL.bg);
+    fa.Wcp = P<u16>(pack, PL.Wc);
+    fa.bc = P<float>(pack, PL.bc);
+    fa.wlo_g = PL.loWg;
+    fa.wlo_c = PL.loWc;
+    fa.Xs = P<float>(ws, L.Xa);
+    for (int t = 0; t <= c.T; ++t) {
+      const float* hin = tr ? P<float>(ws, L.hfT + L.nh4 * t) : (t == 0 && dense) ? h0 : P<float>(ws, L.hf[t & 1]);
+      fa.hf[t] = (t == c.T && dense) ? hT : (float*)hin;
+    }
+    if (tr) {
+      fa.XT = P<u16>(ws, L.XT);
+      fa.hT = P<u16>(ws, L.hT);
+      fa.rhT = P<u16>(ws, L.rhT);
+      fa.r = P<float>(ws, L.r);
+      fa.u = P<float>(ws, L.u);
+      fa.c = P<float>(ws, L.c);
+      fa.sw = (long)(L.nhw / 2);
+      fa.s4 = (long)(L.nh4 / 4);
+    }
+    fa.C = c.C;
+    fa.T = c.T;
+    fa.vsh = c.vsh;
+    fa.sd = c.sdrop;
+    {
+      Prof p(K_FWD_FUSED, s);
+      hipLaunchKernelGGL(k_fwd_fused, dim3(c.b), dim3(512), 0, s, fa);
+    }
+  } else
   for (int t = 0; t < c.T; ++t) {
     const float* hf_in = tr ? P<float>(ws, L.hfT + L.nh4 * t)
                             : (t == 0 && dense) ? h0 : P<float>(ws, L.hf[t & 1]);

@@ -1,0 +1,378 @@
+// k_fused.h -- the whole T-step forward of one graph in one workgroup
+// (hidden 256, v padded to 128, split / fp32-parity mode).
+//
+// Reference: compute_final_node_representations, chem_tensorflow_dense.py:312-340:
+//   for t < T:  X = sum_c A_c (h W_c + beta_c)          (compute_timestep_fast, :391-437)
+//               h = GRUCell(X, h), state dropout         (:237-241, :333)
+// One graph is exactly one 128-row tile, and graphs never interact in the
+// forward, so a workgroup can run every timestep of its graph on its own:
+//   * h stays in LDS between timesteps (f16 hi/lo limb image, chunk-major):
+//     the message transform reads it as the A operand, the GRU reads it as
+//     the h half of its gate product and rewrites it in place with r*h and
+//     then with h';
+//   * X (the aggregated messages) goes to an L2-sized per-graph scratch in
+//     the MFMA accumulator order and comes back as 32-column chunks for the
+//     GRU's two products; it never round-trips through a separate launch;
+//   * the next timestep's first adjacency tile is DMA'd while the blend runs.
+// HBM traffic per graph-step: A (32 KiB per channel), X scratch (L2), the
+// fp32 state, and the activations the backward needs.
+// LDS: image 2 x 64 KiB + 32 KiB shared by the adjacency tile (message
+// passing) and the GRU's two activation ring slots.
+#pragma once
+#include "ggnn_common.h"
+#include "k_gru2.h"
+
+#define FUSED_MAXT 16
+struct FusedFwdArgs {
+  const u16* Ab;                // staged adjacency [b][C][128][128] (k_prep.h layout)
+  const u16* Wp;                // packed edge weights, hi part; lo at +wlo elements
+  long wlo, wstep;              // wstep: elements between per-timestep copies (edge dropout), else 0
+  const float* beta;            // [C][H]
+  const u16* Wgp;               // packed gates kernel (hi; lo at +wlo_g)
+  const float* bg;
+  const u16* Wcp;               // packed candidate kernel (hi; lo at +wlo_c)
+  const float* bc;
+  long wlo_g, wlo_c;
+  float* Xs;                    // X scratch, N*H fp32, accumulator order per graph
+  float* hf[FUSED_MAXT + 1];    // fp32 state [N][H]: hf[t] in, hf[t+1] out
+  u16* XT;                      // training saves (null in inference): X^T, h^T, (r*h)^T
+  u16* hT;                      //   (wg_off layout, stride sw elements per timestep)
+  u16* rhT;
+  float* r;                     //   r, u, c fp32 [N][H] (stride s4 elements per timestep)
+  float* u;
+  float* c;
+  long sw, s4;
+  int C, T, vsh;
+  Drop sd;
+};
+
+__global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
+  using namespace gru2;
+  constexpr int V = 128, VT = 4, ACH = V / 8;
+  typedef Swz<ACH> SA;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 4 * SLOT];
+  char* img_hi = smem;
+  char* img_lo = smem + IMG;
+  char* abuf = smem + 2 * IMG;  // adjacency tile [V][V] (32 KiB) == the GRU ring
+  auto slot_hi = [&](int u) { return smem + 2 * IMG + u * 2 * SLOT; };
+  auto slot_lo = [&](int u) { return smem + 2 * IMG + u * 2 * SLOT + SLOT; };
+
+  const int g = blockIdx.x;
+  const long row0 = (long)g * R;
+  const int C = a.C;
+  const u16* ag = a.Ab + (long)g * C * V * V;
+  float* xs = a.Xs + row0 * H;
+  const rsrc_t rxs = mkrsrc(xs, R * H * 4);
+  const rsrc_t wgh = mkrsrc(a.Wgp, 4 * H * H * 2), wgl = mkrsrc(a.Wgp + a.wlo_g, 4 * H * H * 2);
+  const rsrc_t wch = mkrsrc(a.Wcp, 2 * H * H * 2), wcl = mkrsrc(a.Wcp + a.wlo_c, 2 * H * H * 2);
+
+  // ---- h_0 -> image (limbs); first adjacency tile -> abuf
+  {
+    const int tid = threadIdx.x;
+    const float* h0 = a.hf[0] + row0 * H;
+    for (int q = tid; q < R * (H / 8); q += NT) {
+      const int row = q >> 5, ch = q & 31;
+      const float4 x0 = *(const float4*)(h0 + row * H + ch * 8), x1 = *(const float4*)(h0 + row * H + ch * 8 + 4);
+      const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      st16(img_hi + koff(row, ch), pk8<true>(x));
+      st16(img_lo + koff(row, ch), pk8_lo<true>(x));
+    }
+  }
+  glds_tile<ACH, V, NT>(abuf, ag, (int)threadIdx.x);
+
+  for (int t = 0; t < a.T; ++t) {
+    __syncthreads();  // h_t image complete, A_0 staged (previous blend / prologue)
+    TSMARK(2, 0);
+    // Every lane-derived value is recomputed per timestep from a laundered
+    // thread id: loop-invariant, they would be hoisted out of the T loop
+    // (DMA and chunk addresses, partial Philox rounds) and spilled.
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+    const int n = ns * 32 + l32;
+    const int crow = tid >> 2, cq = tid & 3;
+    const int cso = koff(crow, cq);
+    const int vo = (4 * hh * H + n) * 4;  // this lane's column in a row-major fp32 [R][H] tile
+    // X scratch of this graph, accumulator order: wave w's columns are the
+    // 16 KiB block w (= GRU activation chunk w); a chunk-loader thread reads 8
+    // consecutive lanes' values of one row (32 contiguous bytes)
+    const int xvo_st = (ns * 4096 + lane) * 4;
+    int xvo_ld;
+    {
+      const int it = crow >> 5, rr = crow & 31;
+      const int r = (rr & 3) + 4 * (rr >> 3), h2 = (rr >> 2) & 1;
+      xvo_ld = ((it * 16 + r) * 64 + h2 * 32 + 8 * cq) * 4;
+    }
+    auto xld = [&](int ck) {
+      return Chunk{__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxs, xvo_ld, ck * 16384, kNT)),
+                   __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxs, xvo_ld + 16, ck * 16384, kNT))};
+    };
+    const int vr = ((ns * KSG) * 64 + lane) * 16, vu = (((NS + ns) * KSG) * 64 + lane) * 16;
+    const int vw = ((ns * KS) * 64 + lane) * 16;  // strip ns of a [H][H] pack
+    auto ldg = [&](int k) { return F4{wld(wgh, vr, k), wld(wgl, vr, k), wld(wgh, vu, k), wld(wgl, vu, k)}; };
+    auto ldc = [&](int k) { return F2{wld(wch, vr, k), wld(wcl, vr, k)}; };
+    const long wt = (long)t * a.wstep;
+    const rsrc_t wfh = mkrsrc(a.Wp + wt, C * H * H * 2), wfl = mkrsrc(a.Wp + wt + a.wlo, C * H * H * 2);
+    // ===================== messages: X = sum_c A_c (h W_c + beta_c) =====================
+    f32x16 accx[VT];
+#pragma unroll
+    for (int it = 0; it < VT; ++it) accx[it] = splat(0.f);
+    for (int c = 0; c < C; ++c) {
+      const float bb = a.beta[c * H + n];
+      f32x16 accm[VT];
+#pragma unroll
+      for (int rt = 0; rt < VT; ++rt) accm[rt] = splat(bb);
+      const int cw = c * H * H * 2;
+      auto ldw = [&](int ks) { return F2{bld16(wfh, vw, cw + ks * 1024), bld16(wfl, vw, cw + ks * 1024)}; };
+      b_pipeline<KS, 2>(ldw, [&](int ks, const F2& w) {
+#pragma unroll
+        for (int rt = 0; rt < VT; ++rt) {
+          const int off = koff(rt * 32 + l32, 2 * ks + hh);
+          mma<PREC_SPLIT>(accm[rt], lds_frag(img_hi, off), lds_frag(img_lo, off), w.a, w.b);
+        }
+      });
+      __syncthreads();  // S1: A_c visible
+#pragma unroll
+      for (int rt = 0; rt < VT; ++rt) {
+        const frag mh0 = acc_hi<true>(accm[rt], 0), mh1 = acc_hi<true>(accm[rt], 1);
+        const frag ml0 = acc_lo<true>(accm[rt], 0), ml1 = acc_lo<true>(accm[rt], 1);
+#pragma unroll
+        for (int it = 0; it < VT; ++it) {
+          const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
+          const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
+          mma_xa<PREC_SPLIT>(accx[it], a0, mh0, ml0);
+          mma_xa<PREC_SPLIT>(accx[it], a1, mh1, ml1);
+        }
+      }
+      __syncthreads();  // S2: A_c reads done
+      if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
+    }
+    TSMARK(2, 1);
+    // X -> scratch (accumulator order) and X^T (weight-gradient operand)
+#pragma unroll
+    for (int it = 0; it < VT; ++it)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bst(rxs, accx[it][r], xvo_st, (it * 16 + r) * 256);
+    if (a.XT) {
+      u16* xt = a.XT + t * a.sw;
+#pragma unroll
+      for (int it = 0; it < VT; ++it)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          st_col4w<PREC_SPLIT>(xt + wg_off(n, row0 + it * 32 + 4 * hh, H) + 8 * q, accx[it][4 * q],
+                               accx[it][4 * q + 1], accx[it][4 * q + 2], accx[it][4 * q + 3]);
+    }
+    __syncthreads();  // X visible to every wave
+    TSMARK(2, 2);
+
+    // ============ GRU pass A: [x | h] @ Wg -> r, u; h half first (image) ============
+    f32x16 ar[RT], au[RT];
+    {
+      const float br = a.bg[n], bu = a.bg[H + n];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { ar[rt] = splat(br); au[rt] = splat(bu); }
+    }
+    Chunk st0 = xld(0), st1 = xld(1);
+    F4 w0 = ldg(KS), w1 = ldg(KS + 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ks += 2) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const F4 w = s ? w1 : w0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int off = koff(rt * 32 + l32, 2 * (ks + s) + hh);
+          const frag ah = lds_frag(img_hi, off), al = lds_frag(img_lo, off);
+          mma<PREC_SPLIT>(ar[rt], ah, al, w.a, w.b);
+          mma<PREC_SPLIT>(au[rt], ah, al, w.c, w.d);
+        }
+        const int nk = ks + s + 2;  // runs on into the x rows (k-steps 0, 1)
+        const F4 nw = ldg(nk < KS ? KS + nk : nk - KS);
+        if (s) w1 = nw;
+        else w0 = nw;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    chunk_put(slot_hi(0), slot_lo(0), cso, st0);
+    st0 = xld(2);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NCHK; ++c) {
+      if (c + 1 < NCHK) {
+        chunk_put(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
+        if (c + 3 < NCHK) {
+          if (c & 1) st0 = xld(c + 3);
+          else st1 = xld(c + 3);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ks = 2 * c + s;
+        const F4 w = s ? w1 : w0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int off = koff(rt * 32 + l32, 2 * s + hh);
+          const frag ah = lds_frag(slot_hi(c & 1), off), al = lds_frag(slot_lo(c & 1), off);
+          mma<PREC_SPLIT>(ar[rt], ah, al, w.a, w.b);
+          mma<PREC_SPLIT>(au[rt], ah, al, w.c, w.d);
+        }
+        const F4 nw = ldg(min(ks + 2, KS - 1));
+        if (s) w1 = nw;
+        else w0 = nw;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();
+    }
+    TSMARK(2, 3);
+    // pass B's first x chunks: in flight during the r*h phase
+    st0 = xld(0);
+    st1 = xld(1);
+
+    // ========== r*h in place over the h image; r and (r*h)^T to HBM ==========
+    {
+      const rsrc_t rsr = mkrsrc(a.r ? a.r + t * a.s4 + row0 * H : xs, R * H * 4);
+      u16* rht = a.rhT ? a.rhT + t * a.sw : nullptr;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        float rh[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          au[rt][r] = sigm(au[rt][r]);
+          const float rr = sigm(ar[rt][r]);
+          const int eo = koff(rt * 32 + acc_row(r, hh), n >> 3) + (n & 7) * 2;
+          const float hx = from_limb<true>(*(const u16*)(img_hi + eo)) + from_limb<true>(*(const u16*)(img_lo + eo));
+          rh[r] = rr * hx;
+          *(u16*)(img_hi + eo) = to_limb<true>(rh[r]);
+          *(u16*)(img_lo + eo) = to_limb<true>(lo_part<true>(rh[r]));
+          if (a.r) bst(rsr, rr, vo, (rt * 32 + acc_row0(r)) * H * 4);
+        }
+        if (rht) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            st_col4w<PREC_SPLIT>(rht + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, rh[4 * q], rh[4 * q + 1],
+                                 rh[4 * q + 2], rh[4 * q + 3]);
+        }
+      }
+    }
+    chunk_put(slot_hi(0), slot_lo(0), cso, st0);
+    st0 = xld(2);
+    __syncthreads();
+
+    TSMARK(2, 4);
+    // ============ GRU pass B: [r*h | x] @ [Wc_h ; Wc_x] -> candidate ============
+    f32x16 ac[RT];
+    {
+      const float b0 = a.bc[n];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) ac[rt] = splat(b0);
+    }
+    {
+      F2 v0 = ldc(KS), v1 = ldc(KS + 1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ks += 2) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const F2 w = s ? v1 : v0;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            const int off = koff(rt * 32 + l32, 2 * (ks + s) + hh);
+            mma<PREC_SPLIT>(ac[rt], lds_frag(img_hi, off), lds_frag(img_lo, off), w.a, w.b);
+          }
+          const int nk = ks + s + 2;
+          const F2 nw = ldc(nk < KS ? KS + nk : nk - KS);
+          if (s) v1 = nw;
+          else v0 = nw;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      w0 = F4{v0.a, v0.b, v0.a, v0.b};
+      w1 = F4{v1.a, v1.b, v1.a, v1.b};
+    }
+#pragma unroll
+    for (int c = 0; c < NCHK; ++c) {
+      if (c + 1 < NCHK) {
+        chunk_put(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
+        if (c + 3 < NCHK) {
+          if (c & 1) st0 = xld(c + 3);
+          else st1 = xld(c + 3);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ks = 2 * c + s;
+        const F4 w = s ? w1 : w0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int off = koff(rt * 32 + l32, 2 * s + hh);
+          mma<PREC_SPLIT>(ac[rt], lds_frag(slot_hi(c & 1), off), lds_frag(slot_lo(c & 1), off), w.a, w.b);
+        }
+        const F2 nw = ldc(min(ks + 2, KS - 1));
+        if (s) w1 = F4{nw.a, nw.b, nw.a, nw.b};
+        else w0 = F4{nw.a, nw.b, nw.a, nw.b};
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();  // (last chunk: every r*h / ring read done before the image takes h')
+    }
+    TSMARK(2, 5);
+    // next timestep's first adjacency tile lands while the blend runs
+    if (t + 1 < a.T) glds_tile<ACH, V, NT>(abuf, ag, tid);
+
+    // ===================== blend: h' = u h + (1-u) c, state dropout =====================
+    {
+      const rsrc_t rhp = mkrsrc(a.hf[t] + row0 * H, R * H * 4);
+      const rsrc_t ho = mkrsrc(a.hf[t + 1] + row0 * H, R * H * 4);
+      const bool sav = a.u != nullptr;
+      const rsrc_t uo = mkrsrc(sav ? a.u + t * a.s4 + row0 * H : xs, R * H * 4);
+      const rsrc_t co = mkrsrc(sav ? a.c + t * a.s4 + row0 * H : xs, R * H * 4);
+      u16* hto = (a.hT && t + 1 < a.T) ? a.hT + (t + 1) * a.sw : nullptr;
+      uint4 dw = make_uint4(0, 0, 0, 0);
+      // every h_t load ahead of the first store: vmcnt retires in order, so a
+      // load issued behind a row tile's stores would wait for them to drain
+      float hp[RT][16];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hp[rt][r] = bld(rhp, vo, (rt * 32 + acc_row0(r)) * H * 4);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        float hn[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int so = (rt * 32 + acc_row0(r)) * H * 4;
+          const float cc = tanh_f(ac[rt][r]);
+          const float u = au[rt][r];
+          const float hprev = hp[rt][r];
+          float x = u * hprev + (1.0f - u) * cc;
+          if (a.sd.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
+            if ((r & 3) == 0) {
+              dw = state_words(a.sd, g, rt * 32 + acc_row0(r) + 4 * hh, n, t);
+            }
+            x = drop_apply(a.sd, u4_get(dw, r & 3), x);
+          }
+          hn[r] = x;
+          bst(ho, x, vo, so);
+          if (sav) {
+            bst(uo, u, vo, so);
+            bst(co, cc, vo, so);
+          }
+        }
+        // h' limbs -> image: 8-byte row pieces after a quad transpose
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int eo = koff(rt * 32 + 8 * q + 4 * hh + (l32 & 3), n >> 3) + (n & 4) * 2;
+          const v2u32 wh = quad_transpose4(pk<true>(hn[4 * q], hn[4 * q + 1]), pk<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
+          const v2u32 wl = quad_transpose4(pk_lo<true>(hn[4 * q], hn[4 * q + 1]), pk_lo<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
+          *(uint2*)(img_hi + eo) = make_uint2(wh.x, wh.y);
+          *(uint2*)(img_lo + eo) = make_uint2(wl.x, wl.y);
+        }
+        if (hto) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            st_col4w<PREC_SPLIT>(hto + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, hn[4 * q], hn[4 * q + 1],
+                                 hn[4 * q + 2], hn[4 * q + 3]);
+        }
+      }
+    }
+    TSMARK(2, 6);
+  }
+}

@@ -248,7 +248,7 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
 /* Optional per-kernel timing (HIP events around every launch of the library
  * on the launch's stream), used by bench.py for the roofline.  Not for use
  * under graph capture.  total_ms / launches: arrays of GGNN_NUM_KERNEL_KINDS. */
-#define GGNN_NUM_KERNEL_KINDS 10
+#define GGNN_NUM_KERNEL_KINDS 11
 const char* ggnn_kernel_kind_name(int kind);
 int ggnn_profile_begin(int max_launches);
 int ggnn_profile_end(double* total_ms, int* launches);

@@ -36,10 +36,12 @@ buf = np.zeros((4, 2048, 8), np.uint64)
 assert lib.ggnn_dbg_ts(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 names = {0: ("gru_fwd", 512, ["stage", "passA", "rh", "passB", "blend+st"]),
          1: ("gru_bwd", 512, ["ph1", "prod1", "ph2", "prod2+st"]),
-         2: ("prop_fwd", 256, ["stage", "chan loop", "X out"]),
+         2: ("fwd_fused (last t)", 256, ["msg", "X out", "passA", "rh", "passB", "blend"]),
          3: ("prop_bwd", 256, ["stage", "chan loop", "dh out"])}
 for k, (nm, nwg, phases) in names.items():
     nwg = int((buf[k, :, 0] != 0).sum())
+    if nwg == 0:
+        continue
     t = buf[k, :nwg, :len(phases) + 1].astype(np.int64)
     t0 = t[:, 0].min()
     t = (t - t0) * 0.01  # us
@@ -53,9 +55,3 @@ for k, (nm, nwg, phases) in names.items():
         st = np.sort(t[:, 0])
         print("          start-time quartiles: %s" % np.round(np.percentile(st, [10, 25, 50, 75, 90]), 1))
 
-for k, nm, ph, sl in ((2, "prop_fwd", ["MT", "S1", "AGG", "S2"], [4, 5, 6, 7]),
-                      (3, "prop_bwd", ["ph a+dbeta", "S1", "ph b", "dMT st", "S2"], [4, 5, 6, 3, 7])):
-    nwg = int((buf[k, :, 0] != 0).sum())
-    sums = buf[k, :nwg, sl].astype(np.int64) * 0.01 / 15  # 3 passes x T=5 launches accumulated: us per launch, per WG
-    print("%-8s per-launch channel-loop sums (median over WGs, us, /%d launches): " % (nm, 1) +
-          "  ".join("%s %.1f" % (p, np.median(sums[:, i])) for i, p in enumerate(ph)))
