@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
     const int tid = threadIdx.x;
     const float* h0 = a.hf[0] + row0 * H;
     for (int q = tid; q < R * (H / 8); q += NT) {
-      const int row = q >> 5, ch = q & 31;
+      const int row = q & (R - 1), ch = q >> 7;  // consecutive lanes: consecutive rows of one chunk
       const float4 x0 = *(const float4*)(h0 + row * H + ch * 8), x1 = *(const float4*)(h0 + row * H + ch * 8 + 4);
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
       st16(img_hi + koff(row, ch), pk8<true>(x));
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, ns = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int n = ns * 32 + l32;
-    const int crow = tid >> 2, cq = tid & 3;
+    const int crow = crow_of(tid), cq = cq_of(tid);
     const int cso = koff(crow, cq);
     const int vo = (4 * hh * H + n) * 4;  // this lane's column in a row-major fp32 [R][H] tile
     // X scratch of this graph, accumulator order: wave w's columns are the

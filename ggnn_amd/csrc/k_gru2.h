@@ -41,9 +41,14 @@ DEV uint4 bld16(rsrc_t r, int vo, int so) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
 }
 // one 32-column chunk of a row-major fp32 [R][H] tile: thread tid holds row
-// tid/4, columns 8*(tid%4) .. +8 of the chunk (vo = chunk_vo(tid))
+// crow(tid), columns 8*cq(tid) .. +8 of the chunk (vo = chunk_vo(tid)).  Eight
+// consecutive lanes take eight consecutive rows of one 16-B column piece, so
+// their ds_write_b128 into the chunk-major image is one contiguous 128 B
+// (conflict-free); a wave still covers 16 whole 128-B rows of the chunk.
 struct Chunk { uint4 a, b; };
-DEV int chunk_vo(int tid) { return ((tid >> 2) * H + (tid & 3) * 8) * 4; }
+DEV int crow_of(int tid) { return (tid & 7) + 8 * (tid >> 5); }
+DEV int cq_of(int tid) { return (tid >> 3) & 3; }
+DEV int chunk_vo(int tid) { return (crow_of(tid) * H + cq_of(tid) * 8) * 4; }
 DEV Chunk chunk_ld(rsrc_t r, int vo, int ck) { return Chunk{bld16(r, vo, ck * 128), bld16(r, vo, ck * 128 + 16)}; }
 DEV void chunk_put(char* hi, char* lo, int off, const Chunk& v) {
   const float x[8] = {__uint_as_float(v.a.x), __uint_as_float(v.a.y), __uint_as_float(v.a.z), __uint_as_float(v.a.w),
@@ -74,7 +79,7 @@ k_gru_fwd2(const float* __restrict__ Xa, const float* __restrict__ hf, const u16
   const rsrc_t rx = mkrsrc(Xa + row0 * H, R * H * 4), rhs = mkrsrc(hf + row0 * H, R * H * 4);
   const int cvo = chunk_vo(tid);
   // this thread's 16-B slot in a chunk write (chunk cq of row crow)
-  const int crow = tid >> 2, cq = tid & 3;
+  const int crow = crow_of(tid), cq = cq_of(tid);
   const int cso = koff(crow, cq);
   TSMARK(0, 0);
 

@@ -3,7 +3,7 @@
 # domains mixed in).  Usage (GPU box): bash tools/pmc_profile.sh OUTDIR [bench args]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline --no-side}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0

@@ -51,7 +51,7 @@ for k in sorted(summary):
 if len(sys.argv) > 2:
     kinds = {}
     for k, d in summary.items():
-        m = re.match(r"k_(prop_fwd|prop_bwd|gru_fwd|gru_bwd|wgrad)(?:256)?<", k)
+        m = re.match(r"k_(prop_fwd|prop_bwd|gru_fwd|gru_bwd|wgrad|fwd_fused)(?:256)?(?:<|$)", k)
         if m and "hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d:
             kinds[m.group(1)] = {"kernel": k, "hbm_read_bytes": d["hbm_read_bytes_corrected"],
                                  "hbm_write_bytes": d["hbm_write_bytes"],
