@@ -1,0 +1,109 @@
+"""Host LAS/UAS evaluation of the btb task.
+
+The reference scores each evaluated batch on the host from the heads'
+probabilities (``humanize_batch_results_btb``, chem_tensorflow_dense.py:1160-1215):
+
+* ``get_results_reshaped`` (btb branch, :1054-1079) masks the head / label
+  probabilities and reshapes them to [b, 1, v, o] and [b, e, v, 1];
+* ``adj_mat_to_target`` (:106-131) turns a target 0/1 tensor, or a probability
+  tensor (``is_probability=True``: the arg-max), into a list of
+  ``[source, edge_type]`` per receiving node 1..v-1;
+* ``merge_head_and_edge_graph`` (:1279-1280) joins the head list with the label
+  list; ``get_las_uas`` (:1304-1319) counts exact matches (LAS) and matching
+  heads (UAS, or labels with ``is_edge``).
+
+Pure numpy; no part of the GPU path.  Pinned by the reference's own test vectors
+(``tests_chem.py:9-27, 50-88``) in ``tests/test_evaluation.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def adj_mat_to_target(adj_mat, is_probability=False, true_target=None):
+    """[e, v, o] -> [[source, edge_type], ...] for receiving nodes 1..v-1
+    (chem_tensorflow_dense.py:106-131).  A node whose slice is all zero, or
+    (0/1 input) holds no exact 1, is skipped.  The first maximum in (edge type,
+    source) row-major order wins, as ``np.where(...)[..][0]`` does there.
+    ``true_target`` is accepted for signature parity (only used by a disabled
+    diagnostic in the reference)."""
+    a = np.asarray(adj_mat)
+    num_e, num_v, num_o = a.shape
+    graph = []
+    for node in range(1, num_v):
+        sl = a[:, node, :]
+        mx = np.amax(sl)
+        if mx == 0:
+            continue
+        flat = sl.reshape(-1)
+        hits = np.flatnonzero(flat == (mx if is_probability else 1))
+        if hits.size == 0:
+            continue
+        e, src = divmod(int(hits[0]), num_o)
+        graph.append([src, e + 1])
+    return graph
+
+
+def get_las_uas(target_graph, result_graph, is_edge=False):
+    """Labelled / unlabelled attachment score of one sentence
+    (chem_tensorflow_dense.py:1304-1319).  Edges are [head, label]; UAS compares
+    the head (index 0), or the label (index 1) when ``is_edge``.  Divides by the
+    number of predicted edges, as the reference does."""
+    idx = 1 if is_edge else 0
+    las = uas = 0
+    for i, r in enumerate(result_graph):
+        t = target_graph[i]
+        if t == r:
+            las += 1
+            uas += 1
+        elif t[idx] == r[idx]:
+            uas += 1
+    n = len(result_graph)
+    return las / n, uas / n
+
+
+def merge_head_and_edge_graph(result_graph_l, result_graph_e):
+    """[[head, _]] + [[_, label]] -> [[head, label]] (chem_tensorflow_dense.py:1279-1280)."""
+    return [[x[0], y[1]] for x, y in zip(result_graph_l, result_graph_e)]
+
+
+def results_reshaped_btb(targets, computed_values, mask, num_vertices, output_size, output_size_edges,
+                         is_edge=False):
+    """btb branch of ``get_results_reshaped`` (chem_tensorflow_dense.py:1054-1079):
+    returns (mask, results, targets) as [b, 1, v, o] (heads) or [b, e, v, 1]
+    (labels, ``is_edge``)."""
+    v, e, o = int(num_vertices), int(output_size_edges), int(output_size)
+    cv, m, t = np.asarray(computed_values), np.asarray(mask), np.asarray(targets)
+    if is_edge:
+        res = np.transpose(np.reshape(cv * m, [-1, v, e, 1]), [0, 2, 1, 3])
+        tgt = np.transpose(np.reshape(t, [-1, v, e, 1]), [0, 2, 1, 3])
+        msk = np.transpose(np.reshape(m, [-1, v, e, 1]), [0, 2, 1, 3])
+        return msk, res, tgt
+    return np.reshape(m, [-1, 1, v, o]), np.reshape(cv * m, [-1, 1, v, o]), np.reshape(t, [-1, 1, v, o])
+
+
+def batch_las_uas(labels, computed_values, num_vertices, mask, labels_e, computed_values_e, mask_edges,
+                  output_size, output_size_edges):
+    """Mean (LAS, UAS, label accuracy) over a batch, as
+    ``humanize_batch_results_btb`` computes them (chem_tensorflow_dense.py:1160-1215,
+    without its file output): heads from the arg-max of the head
+    probabilities, labels from the arg-max of the label probabilities."""
+    _, res, tgt = results_reshaped_btb(labels, computed_values, mask, num_vertices, output_size,
+                                       output_size_edges)
+    _, res_e, tgt_e = results_reshaped_btb(labels_e, computed_values_e, mask_edges, num_vertices, output_size,
+                                           output_size_edges, is_edge=True)
+    b = tgt.shape[0]
+    acc_las = acc_uas = acc_uas_e = 0.0
+    for i in range(b):
+        tg_h = adj_mat_to_target(tgt[i])
+        tg_e = adj_mat_to_target(tgt_e[i])
+        target_graph = merge_head_and_edge_graph(tg_h, tg_e)
+        rg_h = adj_mat_to_target(res[i], is_probability=True, true_target=tg_h)
+        rg_e = adj_mat_to_target(res_e[i], is_probability=True)
+        result_graph = merge_head_and_edge_graph(rg_h, rg_e)
+        las, uas = get_las_uas(target_graph, result_graph)
+        _, uas_e = get_las_uas(tg_e, rg_e, is_edge=True)
+        acc_las += las
+        acc_uas += uas
+        acc_uas_e += uas_e
+    return acc_las / b, acc_uas / b, acc_uas_e / b

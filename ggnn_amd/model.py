@@ -15,6 +15,10 @@ chem_tensorflow.py:70-136) that the hot path reads, with the same names:
   fixed_ts=None)`` -> [b, v, h] (:312-340), differentiable: its backward is the
   engine's HIP backward (the reference's TF autodiff, chem_tensorflow.py:496)
 * ``process_raw_graphs`` / ``make_minibatch_iterator`` (``BtbBatching``)
+* ``save_progress`` / ``restore_progress`` in the reference's pickle format
+  (chem_tensorflow.py:796-855; ``checkpoint.py``) and the host LAS/UAS scoring
+  ``get_las_uas`` / ``evaluate_batch`` (chem_tensorflow_dense.py:1160-1215,
+  1304-1319; ``evaluation.py``)
 * the callers either side of the path:
   ``get_initial_node_representation`` (embedding front-end, :264-306),
   ``gated_regression`` + the btb loss (:439-516, chem_tensorflow.py:326-421)
@@ -29,6 +33,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import checkpoint as _ckpt
+from . import evaluation as _eval
 from .batching import BtbBatching
 from .engine import PropagationEngine
 from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
@@ -349,3 +355,43 @@ class DenseGGNNChemModel(BtbBatching):
         sq = [self.lookup_sqnorm.get(id(p)) for p in params]
         self.optimizer.step(grads, grad_scale=grad_scale, sqnorms=sq)
         return loss
+
+    # ------------------------------------------------- checkpoint / evaluation
+    def save_progress(self, model_path: str, train_step: int, valid_step: int) -> None:
+        """chem_tensorflow.py:796-809 (checkpoint.py)."""
+        _ckpt.save_progress(self, model_path, train_step, valid_step)
+
+    def restore_progress(self, model_path: str):
+        """chem_tensorflow.py:816-855 (checkpoint.py); returns (train_step, valid_step)."""
+        return _ckpt.restore_progress(self, model_path)
+
+    get_las_uas = staticmethod(_eval.get_las_uas)  # chem_tensorflow_dense.py:1304-1319
+
+    def evaluate_batch(self, feed_dict=None):
+        """(LAS, UAS, label accuracy) of one batch from the heads' probabilities
+        (``humanize_batch_results_btb``, chem_tensorflow_dense.py:1160-1215):
+        runs the forward + heads (no dropout) and scores on the host."""
+        if feed_dict is not None:
+            self.feed(feed_dict)
+        saved = {k: self.placeholders.get(k) for k in ("out_layer_dropout_keep_prob",)}
+        self.placeholders["out_layer_dropout_keep_prob"] = 1.0
+        try:
+            with torch.no_grad():
+                self.build_loss()
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    self.placeholders.pop(k, None)
+                else:
+                    self.placeholders[k] = v
+        ph = self.placeholders
+        b = int(ph["num_graphs"])
+        v = int(ph["num_vertices"])
+        o, oe = self.params["output_size"], self.output_size_edges
+        probs = self.ops["computed_values"].detach().cpu().numpy()
+        probs_e = self.ops["computed_values_edges"].detach().cpu().numpy()
+        mask = np.asarray(ph["node_mask"], np.float32).reshape(b, v * o)
+        mask_e = np.asarray(ph["node_mask_edges"], np.float32).reshape(b, v * oe)
+        return _eval.batch_las_uas(np.asarray(ph["target_values_head"], np.float32).reshape(b, v * o), probs, v, mask,
+                                   np.asarray(ph["target_values_edges"], np.float32).reshape(b, v * oe), probs_e,
+                                   mask_e, o, oe)

@@ -1,0 +1,135 @@
+"""Host LAS/UAS scoring and the checkpoint format.
+
+The adj_mat_to_target / get_las_uas vectors are the reference's own unit tests
+(tests_chem.py:9-27, 50-88), restated as data.
+"""
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from ggnn_amd import evaluation as E
+from ggnn_amd import checkpoint as K
+from ggnn_amd.model import DenseGGNNChemModel
+
+
+def test_adj_mat_to_target_reference_vector():
+    # tests_chem.py:9-27
+    adj = np.array([[[0., 0., 0., 0., 0.], [0., 0., 0., 1., 0.], [0., 0., 0., 1., 0.], [0., 0., 0., 0., 0.]],
+                    [[0., 0., 0., 0., 0.], [0., 0., 0., 0., 0.], [0., 0., 0., 0., 0.], [1., 0., 0., 0., 0.]]])
+    assert E.adj_mat_to_target(adj_mat=adj) == [[3, 1], [3, 1], [0, 2]]
+
+
+@pytest.mark.parametrize("result,expected", [
+    ([[1, 1], [2, 0], [2, 2]], (1, 1)),        # tests_chem.py:50-58
+    ([[1, 1], [2, 1], [2, 2]], (2 / 3, 1)),    # :60-68
+    ([[1, 0], [2, 1], [2, 1]], (0, 1)),        # :70-78
+    ([[2, 1], [1, 0], [3, 2]], (0, 0)),        # :80-88
+])
+def test_get_las_uas_reference_vectors(result, expected):
+    target = [[1, 1], [2, 0], [2, 2]]
+    assert E.get_las_uas(target_graph=target, result_graph=result) == expected
+    assert DenseGGNNChemModel.get_las_uas(target, result) == expected
+
+
+def test_adj_mat_to_target_probability_first_maximum():
+    rng = np.random.default_rng(0)
+    a = rng.random((3, 6, 6))
+    a[1, 2, 4] = a[2, 2, 0] = 5.0          # tie: (e=1, src=4) comes first in (e, src) order
+    g = E.adj_mat_to_target(a, is_probability=True)
+    assert g[1] == [4, 2]
+    for node, edge in zip(range(1, 6), g):
+        e, src = np.unravel_index(np.argmax(a[:, node, :]), a[:, node, :].shape)
+        assert edge == [int(src), int(e) + 1]
+
+
+def test_batch_las_uas_perfect_and_wrong_predictions():
+    b, v, o, e = 3, 5, 7, 4
+    rng = np.random.default_rng(1)
+    heads = np.zeros((b, v, o), np.float32)
+    labs = np.zeros((b, v, e), np.float32)
+    for g in range(b):
+        for node in range(1, v):
+            heads[g, node, rng.integers(0, v)] = 1
+            labs[g, node, rng.integers(0, e)] = 1
+    mask = np.ones((b, v * o), np.float32)
+    mask_e = np.ones((b, v * e), np.float32)
+    las, uas, le = E.batch_las_uas(heads.reshape(b, -1), heads.reshape(b, -1), v, mask,
+                                   labs.reshape(b, -1), labs.reshape(b, -1), mask_e, o, e)
+    assert (las, uas, le) == (1.0, 1.0, 1.0)
+    wrong = np.roll(labs, 1, axis=2)  # every label wrong, heads right
+    las, uas, le = E.batch_las_uas(heads.reshape(b, -1), heads.reshape(b, -1), v, mask,
+                                   labs.reshape(b, -1), wrong.reshape(b, -1), mask_e, o, e)
+    assert las == 0.0 and uas == 1.0 and le == 0.0
+
+
+def _cpu_model(seed):
+    return DenseGGNNChemModel(params={"hidden_size": 64, "num_timesteps": 2}, num_edge_types=3, device="cpu",
+                              seed=seed, precision="fp32", vocab_size=50, embedding_sizes=dict(loc=16, pos=8, word=24,
+                                                                                                  edge=16))
+
+
+def test_checkpoint_names_follow_the_tf_graph():
+    names = K.variable_names(_cpu_model(0))
+    assert "graph_model/Variable:0" in names and "graph_model/Variable_3:0" in names
+    assert tuple(names["graph_model/Variable:0"].shape) == (6, 64, 64)          # edge_weights [2E, h, h]
+    assert tuple(names["graph_model/Variable_1:0"].shape) == (6, 1, 64)         # edge_biases
+    assert tuple(names["graph_model/gru_scope/gru_cell/gates/kernel:0"].shape) == (128, 128)
+    assert "out_layer_task0/regression_gate/MLP_W_layer0_1:0" in names
+    assert "graph_model/word_embedding:0" in names
+
+
+class _FakeAdam:  # ClipAdam's state attributes (the real one needs a GPU)
+    def __init__(self, params):
+        self.params = params
+        self.m = [torch.full_like(p, 0.25) for p in params]
+        self.v = [torch.full_like(p, 0.5) for p in params]
+        self.b1, self.b2, self.t = 0.9, 0.999, 7
+
+
+def test_checkpoint_round_trip(tmp_path):
+    a, b = _cpu_model(0), _cpu_model(1)
+    a.optimizer = _FakeAdam(a.trainable_variables())
+    b.optimizer = _FakeAdam(b.trainable_variables())
+    for m in b.optimizer.m:
+        m.zero_()
+    b.optimizer.t = 0
+    path = os.path.join(tmp_path, "model.pickle")
+    a.save_progress(path, train_step=11, valid_step=4)
+    with open(path, "rb") as f:
+        data = pickle.load(f)  # our own file
+    assert set(data) == {"params", "weights", "train_step", "valid_step"}
+    assert data["params"]["hidden_size"] == 64
+    assert "graph_model/Variable/Adam:0" in data["weights"] and "beta1_power:0" in data["weights"]
+    logs = []
+    assert K.restore_progress(b, path, log=logs.append) == (11, 4)
+    for n, t in K.variable_names(a).items():
+        assert torch.equal(t, K.variable_names(b)[n]), n
+    assert all(torch.all(m == 0.25) for m in b.optimizer.m) and b.optimizer.t == 7
+    assert not logs
+
+
+def test_checkpoint_restore_tolerates_missing_and_reports_unused(tmp_path):
+    a = _cpu_model(0)
+    path = os.path.join(tmp_path, "m.pickle")
+    a.save_progress(path, 1, 2)
+    with open(path, "rb") as f:
+        data = pickle.load(f)
+    del data["weights"]["graph_model/word_embedding:0"]
+    data["weights"]["graph_model/att_weights_extra:0"] = np.zeros(3, np.float32)
+    with open(path, "wb") as f:
+        pickle.dump(data, f)
+    b = _cpu_model(5)
+    before = b.weights["word_embeddings"].detach().clone()
+    logs = []
+    K.restore_progress(b, path, log=logs.append)
+    assert torch.equal(b.weights["word_embeddings"], before)
+    assert any("Freshly initializing graph_model/word_embedding:0" in s for s in logs)
+    assert any("att_weights_extra" in s for s in logs)
+    data["weights"]["graph_model/Variable:0"] = np.zeros((2, 2), np.float32)
+    with open(path, "wb") as f:
+        pickle.dump(data, f)
+    with pytest.raises(ValueError):
+        K.restore_progress(b, path, log=logs.append)

@@ -190,3 +190,30 @@ def test_model_trains_on_dev_batches():
     losses = [float(m.train_step(fd).detach()) for _ in range(8)]
     assert np.isfinite(losses).all()
     assert losses[-1] < 0.9 * losses[0]
+
+
+@pytest.mark.gpu
+def test_evaluate_batch_las_uas_and_checkpoint_resume(tmp_path):
+    """Host LAS/UAS of the drop-in model on real dev batches
+    (chem_tensorflow_dense.py:1160-1215) improves when the model fits a batch,
+    and a checkpoint written mid-training resumes to the same next step
+    (chem_tensorflow.py:796-855)."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=True)
+    fd = feeds[0]
+    las0, uas0, le0 = m.evaluate_batch(fd)
+    assert 0.0 <= las0 <= uas0 <= 1.0 and 0.0 <= le0 <= 1.0
+    for _ in range(25):
+        m.train_step(fd)
+    las1, uas1, le1 = m.evaluate_batch(fd)
+    assert uas1 > uas0 and las1 >= las0
+    path = str(tmp_path / "model.pickle")
+    m.save_progress(path, train_step=25, valid_step=0)
+    m2, _ = _dev_model(torch, keep_all=True)
+    m2.feed(fd)
+    m2.train_step(fd)  # creates the optimizer state that the restore overwrites
+    assert m2.restore_progress(path) == (25, 0)
+    for _ in range(2):  # the second loss sees one Adam update from the restored state
+        l_a = float(m.train_step(fd).detach())
+        l_b = float(m2.train_step(fd).detach())
+        assert abs(l_a - l_b) <= 1e-5 * max(1.0, abs(l_a))
