@@ -225,8 +225,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    const rsrc_t rdm = mkrsrc(dMT + (long)c * H * N, 0x7fffffff);
-    const int vm = (int)(wg_off(ns * 32 + 4 * hh + (l32 & 3), rowg + 4 * (l32 >> 2), H) * 2);
     auto ldb = [&](int ks) {
       return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
     };
@@ -244,12 +242,28 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     // weight-fragment wait of the channel: vmcnt is in order, so a store ahead of
     // a load would make that load's wait cover the store too.  The stores then
     // drain during the next channel's phase a, which has no vector-memory loads.
+    // 16 contiguous bytes per lane: lanes l and l^4 hold neighbouring 4-row
+    // pieces of the same columns for quads q and q+1; one ds_swizzle exchange
+    // gives the even lane both pieces of quad q and the odd lane both of q+1
+    // (8-byte stores are issue-bound: ~7 B/cycle/CU, 16-byte ones about twice
+    // that).  global_store, not buffer_store: the raw-buffer dwordx4 store read
+    // its data VGPRs late (DESIGN.md §4 lessons).
     if (dMT) {
+      const bool odd = (l32 >> 2) & 1;
+      u16* dmt = dMT + (long)c * H * N;
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          __builtin_amdgcn_raw_buffer_store_b64(dq[jt][q], rdm, vm + jt * 64 * H, 8 * q * 64, kNT);
+        for (int qp = 0; qp < 4; qp += 2) {
+          const v2u32 mine = odd ? dq[jt][qp + 1] : dq[jt][qp];
+          const v2u32 send = odd ? dq[jt][qp] : dq[jt][qp + 1];
+          const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send.x, 0x101F);  // lane ^ 4
+          const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send.y, 0x101F);
+          typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+          const u32x4v out = odd ? u32x4v{r0, r1, mine.x, mine.y} : u32x4v{mine.x, mine.y, r0, r1};
+          const int nn = ns * 32 + 8 * (qp + (odd ? 1 : 0)) + 4 * hh + (l32 & 3);
+          __builtin_nontemporal_store(out, (u32x4v*)(dmt + wg_off(nn, rowg + jt * 32 + 8 * (l32 >> 3), H)));
+        }
     }
     __syncthreads();  // S2: dM image reads done, A_{c+1} staged
   }
