@@ -31,10 +31,13 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = V * H * 2;
   constexpr int A_BYTES = V * V * 2;
-  __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + A_BYTES];
+  // two adjacency tiles where the LDS has room (16-bit modes): A_{c+1} is
+  // DMA'd right after channel c's only barrier, into the tile AGG(c-1) read
+  constexpr int NAB = (!SPLIT && NIMG * IMG + 2 * A_BYTES <= 163840) ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + NAB * A_BYTES];
   char* h_hi = smem;
   char* h_lo = smem + (SPLIT ? IMG : 0);
-  char* abuf = smem + NIMG * IMG;
+  auto abuf_of = [&](int c) { return smem + NIMG * IMG + (NAB == 2 ? (c & 1) * A_BYTES : 0); };
 
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, ns = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -43,8 +46,9 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 
   stage_rows<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
-  glds_tile<ACH, V, NT>(abuf, ag, tid);
+  glds_tile<ACH, V, NT>(abuf_of(0), ag, tid);
   __syncthreads();
+  if (NAB == 2 && C > 1) glds_tile<ACH, V, NT>(abuf_of(1), ag + (long)V * V, tid);
 
   f32x16 accx[VT];
 #pragma unroll
@@ -73,7 +77,9 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     // fully unrolled direct loop in the single-product modes
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
-    __syncthreads();  // S1: A_c visible
+    __syncthreads();  // S1: A_c visible (two tiles: and every wave is past AGG(c-1))
+    if (NAB == 2 && c >= 1 && c + 1 < C) glds_tile<ACH, V, NT>(abuf_of(c + 1), ag + (long)(c + 1) * V * V, tid);
+    const char* abuf = abuf_of(c);
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
     for (int rt = 0; rt < VT; ++rt) {
@@ -87,9 +93,11 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
         mma_xa<PREC>(accx[it], a1, mh1, ml1);
       }
     }
-    __syncthreads();  // S2: A_c reads done
-    // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
-    if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
+    if constexpr (NAB == 1) {
+      __syncthreads();  // S2: A_c reads done
+      // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
+      if (c + 1 < C) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)(c + 1) * V * V, tid);
+    }
   }
 
   // ---- X^T (transposed, weight-gradient operand)
@@ -101,7 +109,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
         st_col4w<PREC>(XT + wg_off(n, rowg + it * 32 + 4 * hh, H) + 8 * q, accx[it][4 * q], accx[it][4 * q + 1],
                        accx[it][4 * q + 2], accx[it][4 * q + 3]);
   }
-  // ---- X row-major through LDS (the h images are free after the last S2)
+  // ---- X row-major through LDS (the h images are free once every wave is past the last MT)
   if constexpr (SPLIT) {
     float* xs = (float*)smem;  // [V][H] fp32 = NIMG*IMG bytes
 #pragma unroll
