@@ -310,6 +310,28 @@ DEV void stage_rows(char* hi, char* lo, const ActT<PREC>* src, long ld, int tid)
   }
 }
 
+// ---- chunk-major LDS image of R rows: 16-byte chunk ch (8 consecutive k) of
+// row r at ch * (R * 16) + r * 16.  A fragment read (16 lanes = 16 rows of one
+// chunk) is 256 contiguous bytes, and its k offset is an immediate.
+template <int R> DEV int kimg(int row, int ch) { return ch * (R * 16) + row * 16; }
+// block-cooperative staging into chunk-major image(s); consecutive lanes take
+// consecutive rows of one chunk (conflict-free 16-byte LDS writes)
+template <int PREC, int R, int K, int NT>
+DEV void stage_rows_k(char* hi, char* lo, const ActT<PREC>* src, long ld, int tid) {
+  for (int q = tid; q < R * (K / 8); q += NT) {
+    const int row = q % R, ch = q / R;
+    if constexpr (Prec<PREC>::split) {
+      const float4 a = *(const float4*)(src + row * ld + ch * 8);
+      const float4 b = *(const float4*)(src + row * ld + ch * 8 + 4);
+      const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      st16(hi + kimg<R>(row, ch), pk8<true>(x));
+      st16(lo + kimg<R>(row, ch), pk8_lo<true>(x));
+    } else {
+      st16(hi + kimg<R>(row, ch), ld16(src + row * ld + ch * 8));
+    }
+  }
+}
+
 // ---- store 4 consecutive rows (acc regs 4q..4q+3) of one column into a
 // transposed [col][row] activation array (rows contiguous)
 template <int PREC>

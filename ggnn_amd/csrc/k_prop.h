@@ -44,7 +44,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   const int n = ns * 32 + l32;
   const long rowg = (long)g * V;
 
-  stage_rows<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
+  stage_rows_k<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
   glds_tile<ACH, V, NT>(abuf_of(0), ag, tid);
   __syncthreads();
@@ -67,7 +67,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     auto mt = [&](int ks, const F2& w) {
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
-        const int off = SH::off(rt * 32 + l32, 2 * ks + hh);
+        const int off = kimg<V>(rt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(h_hi, off);
         const frag al = SPLIT ? lds_frag(h_lo, off) : ah;
         mma<PREC>(accm[rt], ah, al, w.a, w.b);
@@ -122,11 +122,11 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 #pragma unroll
     for (int it = 0; it < VT; ++it)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) *(u16*)(h_hi + SH::eoff(it * 32 + acc_row(r, hh), n)) = to_limb<F16>(accx[it][r]);
+      for (int r = 0; r < 16; ++r) *(u16*)(h_hi + kimg<V>(it * 32 + acc_row(r, hh), n >> 3) + (n & 7) * 2) = to_limb<F16>(accx[it][r]);
     __syncthreads();
     for (int q = tid; q < V * HCH; q += NT) {
       const int row = q / HCH, ch = q % HCH;
-      st16(Xo + (rowg + row) * H + ch * 8, ld16(h_hi + SH::off(row, ch)));
+      st16(Xo + (rowg + row) * H + ch * 8, ld16(h_hi + kimg<V>(row, ch)));
     }
   }
 }
