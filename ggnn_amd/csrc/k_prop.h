@@ -26,7 +26,6 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KS = H / 16;
   constexpr int HCH = H / 8, ACH = V / 8;
-  typedef Swz<HCH> SH;
   typedef Swz<ACH> SA;
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = V * H * 2;
@@ -205,9 +204,10 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       for (int q = 0; q < 4; ++q) {
         const int n0 = ns * 32 + 8 * q + 4 * hh;
         const uint32_t p0 = pk<F16>(am[4 * q], am[4 * q + 1]), p1 = pk<F16>(am[4 * q + 2], am[4 * q + 3]);
-        *(uint2*)(m_hi + SH::eoff(j, n0)) = make_uint2(p0, p1);
+        const int mo = kimg<V>(j, n0 >> 3) + (n0 & 7) * 2;  // chunk-major dM image
+        *(uint2*)(m_hi + mo) = make_uint2(p0, p1);
         if constexpr (SPLIT)
-          *(uint2*)(m_lo + SH::eoff(j, n0)) =
+          *(uint2*)(m_lo + mo) =
               make_uint2(pk_lo<true>(am[4 * q], am[4 * q + 1]), pk_lo<true>(am[4 * q + 2], am[4 * q + 3]));
         dq[jt][q] = quad_transpose4(p0, p1, l32 & 3);
       }
@@ -239,7 +239,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     auto pb = [&](int ks, const F2& w) {
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt) {
-        const int off = SH::off(jt * 32 + l32, 2 * ks + hh);
+        const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(m_hi, off);
         const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
         mma<PREC>(adh[jt], ah, al, w.a, SPLIT ? w.b : w.a);
