@@ -242,6 +242,16 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10)
             "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
 
 
+def load_ceilings():
+    """Library MFMA / copy ceilings measured on the box (tools/ceilings.py)."""
+    p = os.path.join(ROOT, "profiles", "ceilings.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
 def load_traffic():
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -373,11 +383,22 @@ def main():
     roof = {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / BF16_DENSE_PEAK_TFLOPS) if achieved else None,
             "traffic": traffic, "avg_launch_ms": avg_ms, "algo_flops_per_launch": fl}
+    ceil = load_ceilings()
+    if ceil:
+        # library ceilings measured on an MI355X box (tools/ceilings.py): the
+        # f16 GEMM for the f16 / fp32-parity limbs, the bf16 GEMM for bf16
+        key = "gemm_bf16_tflops" if args.precision == "bf16" else "gemm_f16_tflops"
+        roof["measured_peak"] = ceil[key]
+        roof["measured_peak_source"] = "profiles/ceilings.json (%s, hipBLASLt 8192^3)" % key
+        if achieved:
+            roof["frac_of_measured"] = achieved / ceil[key]
     ifl = kernel_issued_flops(dom, b, v, h, C, T, args.precision)
     if ifl and avg_ms:
         # the MFMA pipes' real load: issued products (limb split included) / peak
         roof["issued_flops_per_launch"] = ifl
         roof["frac_issued"] = ifl / (avg_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS
+        if ceil:
+            roof["frac_issued_of_measured"] = ifl / (avg_ms * 1e-3) / 1e12 / roof["measured_peak"]
     breakdown = {k: {"ms_per_step": timer.total_ms[k] / args.steps, "launches_per_step": timer.launches[k] / args.steps}
                  for k in kinds}
 
