@@ -89,26 +89,40 @@ def cpu_baseline(seconds=10.0, sample_b=8):
         threadpool_limits = None
     cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     C = 2 * CFG["e"]
-    A, h0 = O.synthetic_batch(sample_b, CFG["v"], CFG["h"], C, seed=1)
-    w = O.synthetic_weights(CFG["h"], C, seed=1, parity_bias=False)
-    dhT = np.ones_like(h0)
-    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+
+    def run(threads, secs, gb):
+        A, h0 = O.synthetic_batch(gb, CFG["v"], CFG["h"], C, seed=1)
+        w = O.synthetic_weights(CFG["h"], C, seed=1, parity_bias=False)
+        dhT = np.ones_like(h0)
+        ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+        try:
+            n = 0
+            t0 = time.perf_counter()
+            while True:
+                hT, caches = O.forward(A, h0, w, CFG["T"])
+                O.backward(A, dhT, caches, w)
+                n += gb
+                el = time.perf_counter() - t0
+                if el >= secs:
+                    break
+        finally:
+            if ctx is not None and hasattr(ctx, "restore_original_limits"):
+                ctx.restore_original_limits()
+        return n / el, "oracle fp32 numpy fwd+bwd, %d graphs/batch (v=%d h=%d C=%d T=%d), %d graphs in %.1f s" % (
+            gb, CFG["v"], CFG["h"], C, CFG["T"], n, el)
+
+    value, sample = run(cores, seconds, sample_b)
+    # all cores and one core, CPU model stated (the 1-core leg is a
+    # short sample of 2-graph batches so the default bench stays within minutes)
+    v1, s1 = run(1, max(2.0, seconds / 3), 2)
+    model = None
     try:
-        n = 0
-        t0 = time.perf_counter()
-        while True:
-            hT, caches = O.forward(A, h0, w, CFG["T"])
-            O.backward(A, dhT, caches, w)
-            n += sample_b
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
-    finally:
-        if ctx is not None:
-            ctx.unregister() if hasattr(ctx, "unregister") else None
-    return dict(value=n / el, unit="graphs/s", cores=cores, kind="port",
-                sample="oracle fp32 numpy fwd+bwd, %d graphs/batch (v=%d h=%d C=%d T=%d), %d graphs in %.1f s"
-                       % (sample_b, CFG["v"], CFG["h"], C, CFG["T"], n, el))
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
+    return dict(value=value, unit="graphs/s", cores=cores, kind="port", sample=sample, cpu_model=model,
+                single_core=dict(value=v1, unit="graphs/s", cores=1, sample=s1))
 
 
 def adjacency_feed_costs(eng, b, v, E, dev, reps=5):
