@@ -332,6 +332,24 @@ DEV void stage_rows_k(char* hi, char* lo, const ActT<PREC>* src, long ld, int ti
   }
 }
 
+// Saved GRU activations r, u, c (fp32, written by the GRU forward kernels and
+// read only by k_gru_bwd) are stored row-quad-major: element (row, n) sits at
+// float ((row >> 2) * H + n) * 4 + (row & 3).  The 4 consecutive rows an MFMA
+// accumulator quad holds (registers 4q..4q+3) are 16 contiguous bytes: one
+// dwordx4 per quad, no cross-lane shuffle.  Offsets are relative to the row
+// tile's base pointer (first row a multiple of 4).
+DEV int qm_vo(int hh, int n, int H) { return (hh * H + n) * 16; }
+DEV int qm_so(int rt, int q, int H) { return (8 * rt + 2 * q) * H * 16; }
+// 16-byte global store, saddr form (wave-uniform base + soff, 32-bit lane
+// offset).  Not buffer_store_dwordx4: that store read its data VGPRs after a
+// following instruction had rewritten them (DESIGN.md §4 lessons).
+DEV void gst4(void* base, int voff, int soff, float4 v) {
+  *(float4*)((char*)base + soff + (unsigned long)(unsigned)voff) = v;
+}
+DEV float4 bld4(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 // ---- store 4 consecutive rows (acc regs 4q..4q+3) of one column into a
 // transposed [col][row] activation array (rows contiguous)
 template <int PREC>

@@ -230,21 +230,26 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 
     // ========== r*h in place over the h image; r and (r*h)^T to HBM ==========
     {
-      const rsrc_t rsr = mkrsrc(a.r ? a.r + t * a.s4 + row0 * H : xs, R * H * 4);
       u16* rht = a.rhT ? a.rhT + t * a.sw : nullptr;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        float rh[16];
+        float rh[16], rv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           au[rt][r] = sigm(au[rt][r]);
           const float rr = sigm(ar[rt][r]);
+          rv[r] = rr;
           const int eo = koff(rt * 32 + acc_row(r, hh), n >> 3) + (n & 7) * 2;
           const float hx = from_limb<true>(*(const u16*)(img_hi + eo)) + from_limb<true>(*(const u16*)(img_lo + eo));
           rh[r] = rr * hx;
           *(u16*)(img_hi + eo) = to_limb<true>(rh[r]);
           *(u16*)(img_lo + eo) = to_limb<true>(lo_part<true>(rh[r]));
-          if (a.r) bst(rsr, rr, vo, (rt * 32 + acc_row0(r)) * H * 4);
+        }
+        if (a.r) {  // row-quad-major save (ggnn_common.h: qm_vo)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            gst4(a.r + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+                 make_float4(rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]));
         }
         if (rht) {
 #pragma unroll
@@ -322,8 +327,6 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       const rsrc_t rhp = mkrsrc(a.hf[t] + row0 * H, R * H * 4);
       const rsrc_t ho = mkrsrc(a.hf[t + 1] + row0 * H, R * H * 4);
       const bool sav = a.u != nullptr;
-      const rsrc_t uo = mkrsrc(sav ? a.u + t * a.s4 + row0 * H : xs, R * H * 4);
-      const rsrc_t co = mkrsrc(sav ? a.c + t * a.s4 + row0 * H : xs, R * H * 4);
       u16* hto = (a.hT && t + 1 < a.T) ? a.hT + (t + 1) * a.sw : nullptr;
       uint4 dw = make_uint4(0, 0, 0, 0);
       // every h_t load ahead of the first store: vmcnt retires in order, so a
@@ -335,7 +338,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         for (int r = 0; r < 16; ++r) hp[rt][r] = bld(rhp, vo, (rt * 32 + acc_row0(r)) * H * 4);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        float hn[16];
+        float hn[16], uv[16], cv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int so = (rt * 32 + acc_row0(r)) * H * 4;
@@ -351,9 +354,16 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
           }
           hn[r] = x;
           bst(ho, x, vo, so);
-          if (sav) {
-            bst(uo, u, vo, so);
-            bst(co, cc, vo, so);
+          uv[r] = u;
+          cv[r] = cc;
+        }
+        if (sav) {  // row-quad-major saves
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            gst4(a.u + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+                 make_float4(uv[4 * q], uv[4 * q + 1], uv[4 * q + 2], uv[4 * q + 3]));
+            gst4(a.c + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+                 make_float4(cv[4 * q], cv[4 * q + 1], cv[4 * q + 2], cv[4 * q + 3]));
           }
         }
         // h' limbs -> image: 8-byte row pieces after a quad transpose

@@ -113,10 +113,11 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
           st_col4w<PREC>(rhT_out + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, rh[4 * q], rh[4 * q + 1],
                          rh[4 * q + 2], rh[4 * q + 3]);
       }
-      if (r_out) {
-        const rsrc_t ro = mkrsrc(r_out + row0 * H, R * H * 4);
+      if (r_out) {  // row-quad-major save
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bst(ro, ar[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
+        for (int q = 0; q < 4; ++q)
+          gst4(r_out + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+               make_float4(ar[rt][4 * q], ar[rt][4 * q + 1], ar[rt][4 * q + 2], ar[rt][4 * q + 3]));
       }
     }
   }
@@ -150,6 +151,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
   if constexpr (!SPLIT) __syncthreads();  // the h image is reused to stage h' (bf16) below
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
+    float u4[4], c4[4], r4[4];  // one accumulator quad of u, c, r (row-quad-major saves)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int so = (rt * 32 + acc_row0(r)) * H * 4;
@@ -168,9 +170,15 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
       }
       bst(ho, hn, vo, so);
       if (u_out) {
-        bst(mkrsrc(u_out + row0 * H, R * H * 4), u, vo, so);
-        bst(mkrsrc(c_out + row0 * H, R * H * 4), cc, vo, so);
-        if constexpr (DEFER) bst(mkrsrc(r_out + row0 * H, R * H * 4), ar[rt][r], vo, so);
+        u4[r & 3] = u;
+        c4[r & 3] = cc;
+        r4[r & 3] = ar[rt][r];
+        if ((r & 3) == 3) {
+          const int qo = qm_so(rt, r >> 2, H), qv = qm_vo(hh, n, H);
+          gst4(u_out + row0 * H, qv, qo, make_float4(u4[0], u4[1], u4[2], u4[3]));
+          gst4(c_out + row0 * H, qv, qo, make_float4(c4[0], c4[1], c4[2], c4[3]));
+          if constexpr (DEFER) gst4(r_out + row0 * H, qv, qo, make_float4(r4[0], r4[1], r4[2], r4[3]));
+        }
       }
       if (DEFER && rhT_out) au[rt][r] = ar[rt][r] * hprev;  // r*h (u is dead from here)
       ac[rt][r] = hn;
@@ -244,11 +252,13 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float dz[4], zu[4];
+      const float4 u4 = bld4(pu, qm_vo(hh, n, H), qm_so(rt, q, H)), c4 = bld4(pc, qm_vo(hh, n, H), qm_so(rt, q, H));
+      const float uq[4] = {u4.x, u4.y, u4.z, u4.w}, cq[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld(pd, vo, so), u = bld(pu, vo, so), c = bld(pc, vo, so), h = bld(ph, vo, so);
+        const float d = bld(pd, vo, so), u = uq[i], c = cq[i], h = bld(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
         du[rt][4 * q + i] = d * u;
@@ -295,12 +305,14 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float zr[4];
+      const float4 r4 = bld4(pr, qm_vo(hh, n, H), qm_so(rt, q, H));
+      const float rq[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * q + i;
         const int ro = rt * 32 + acc_row0(r);
         const int so = ro * H * 4;
-        const float h = bld(ph, vo, so), rr = bld(pr, vo, so);
+        const float h = bld(ph, vo, so), rr = rq[i];
         const float drh = a2[rt][r];
         a2[rt][r] = du[rt][r] + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);

@@ -142,21 +142,25 @@ k_gru_fwd2(const float* __restrict__ Xa, const float* __restrict__ hf, const u16
 
   // ========== r*h in place over the h image; r and (r*h)^T to HBM ==========
   const int vo = (4 * hh * H + n) * 4;
-  const rsrc_t rsr = mkrsrc(r_out ? r_out + row0 * H : hf_out, R * H * 4);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    float rh[16];
+    float rh[16], rv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       au[rt][r] = sigm(au[rt][r]);
       const float rr = sigm(ar[rt][r]);
+      rv[r] = rr;
       const int row = rt * 32 + acc_row(r, hh);
       const int eo = koff(row, n >> 3) + (n & 7) * 2;
       const float hx = from_limb<true>(*(const u16*)(img_hi + eo)) + from_limb<true>(*(const u16*)(img_lo + eo));
       rh[r] = rr * hx;
       *(u16*)(img_hi + eo) = to_limb<true>(rh[r]);
       *(u16*)(img_lo + eo) = to_limb<true>(lo_part<true>(rh[r]));
-      if (r_out) bst(rsr, rr, vo, (rt * 32 + acc_row0(r)) * H * 4);
+    }
+    if (r_out) {  // row-quad-major save
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gst4(r_out + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H), make_float4(rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]));
     }
     if (rhT_out) {
 #pragma unroll
@@ -235,11 +239,13 @@ k_gru_fwd2(const float* __restrict__ Xa, const float* __restrict__ hf, const u16
   uint4 dw = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    float hn[16];
+    float hn[16], uv[16], cv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int so = (rt * 32 + acc_row0(r)) * H * 4;
       const float cc = tanh_f(ac[rt][r]);
+      uv[r] = au[rt][r];
+      cv[r] = cc;
       const float u = au[rt][r];
       const float hprev = bld(rhs, vo, so);
       float x = u * hprev + (1.0f - u) * cc;
@@ -252,9 +258,12 @@ k_gru_fwd2(const float* __restrict__ Xa, const float* __restrict__ hf, const u16
       }
       hn[r] = x;
       bst(ho, x, vo, so);
-      if (u_out) {
-        bst(mkrsrc(u_out + row0 * H, R * H * 4), u, vo, so);
-        bst(mkrsrc(c_out + row0 * H, R * H * 4), cc, vo, so);
+    }
+    if (u_out) {  // row-quad-major saves
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        gst4(u_out + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H), make_float4(uv[4 * q], uv[4 * q + 1], uv[4 * q + 2], uv[4 * q + 3]));
+        gst4(c_out + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H), make_float4(cv[4 * q], cv[4 * q + 1], cv[4 * q + 2], cv[4 * q + 3]));
       }
     }
     if (hT_out) {
