@@ -423,6 +423,25 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
 template <int PREC>
 int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, float* dWc, hipStream_t s);
 
+// gradient accumulators zeroed by grouped k_zero_multi launches (flushed when
+// the job table fills and on scope exit)
+struct Zeroer {
+  hipStream_t s;
+  ZeroJobs j;
+  int n = 0;
+  explicit Zeroer(hipStream_t st) : s(st) {}
+  void add(float* p, long cnt) {
+    if (cnt <= 0) return;
+    j.p[n] = p, j.n[n] = cnt;
+    if (++n == ZERO_MAXJ) flush();
+  }
+  void flush() {
+    if (n) hipLaunchKernelGGL(k_zero_multi, dim3(256, n), dim3(256), 0, s, j);
+    n = 0;
+  }
+  ~Zeroer() { flush(); }
+};
+
 template <int PREC>
 int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, const float* dhT, float* dh0, float* dW,
                   float* dbeta, float* dWg, float* dbg, float* dWc, float* dbc, hipStream_t s) {
@@ -433,14 +452,17 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
 
-  HIPCHK(hipMemsetAsync(dW, 0, (size_t)c.C * H * H * 4, s));
-  HIPCHK(hipMemsetAsync(dWg, 0, (size_t)4 * H * H * 4, s));
-  HIPCHK(hipMemsetAsync(dbg, 0, (size_t)2 * H * 4, s));
-  HIPCHK(hipMemsetAsync(dWc, 0, (size_t)2 * H * H * 4, s));
-  HIPCHK(hipMemsetAsync(dbc, 0, (size_t)H * 4, s));
-  if (c.ed) HIPCHK(hipMemsetAsync(P<float>(ws, L.G), 0, (size_t)c.T * c.C * H * H * 4, s));
-
-  if (use_bias) HIPCHK(hipMemsetAsync(dbeta, 0, (size_t)c.C * H * 4, s));
+  {
+    Prof p(K_IO, s);
+    Zeroer z(s);
+    z.add(dW, (long)c.C * H * H);
+    z.add(dWg, 4 * H * H);
+    z.add(dbg, 2 * H);
+    z.add(dWc, 2 * H * H);
+    z.add(dbc, H);
+    if (c.ed) z.add(P<float>(ws, L.G), (long)c.T * c.C * H * H);
+    if (use_bias) z.add(dbeta, (long)c.C * H);
+  }
   float* dA = P<float>(ws, L.dA);
   float* dB = P<float>(ws, L.dB);
   // unpadded batch without state dropout: dL/dh_T is read in place and the
@@ -903,10 +925,13 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
   for (int i = 0; i < nseg; ++i) {
     if (!segs[i].d_table) return fail(GGNN_EINVAL, "embed_backward: NULL d_table");
     gd.dtable[i] = segs[i].d_table;
-    HIPCHK(hipMemsetAsync(segs[i].d_table, 0, (size_t)segs[i].rows * segs[i].width * 4, s));
   }
-  HIPCHK(hipMemsetAsync(lookup_sqnorm, 0, (size_t)nseg * 4, s));
   Prof p(K_HEADS, s);
+  {
+    Zeroer z(s);
+    for (int i = 0; i < nseg; ++i) z.add(segs[i].d_table, (long)segs[i].rows * segs[i].width);
+    z.add(lookup_sqnorm, nseg);
+  }
   hipLaunchKernelGGL(k_embed_bwd, dim3(std::min(grid1d(a.rows * a.H), 4096)), dim3(256), 0, s, a, gd, word_inputs,
                      dh0, dh0_add, lookup_sqnorm);
   LAUNCHCHK();
@@ -987,6 +1012,13 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
     if (!heads[i].labels || !heads[i].probs || !heads[i].d_weight || !heads[i].d_bias)
       return fail(GGNN_EINVAL, "heads_backward: head needs labels, probs, d_weight, d_bias");
   Prof p(K_HEADS, s);
+  {
+    Zeroer z(s);
+    for (int i = 0; i < nheads; ++i) {
+      z.add(heads[i].d_weight, (long)K * heads[i].o);
+      z.add(heads[i].d_bias, heads[i].o);
+    }
+  }
   for (int i = 0; i < nheads; ++i) {
     const ggnn_output_head& hd = heads[i];
     const int o = hd.o;
@@ -996,8 +1028,6 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
     HeadDxP q{dZ, P<const float>(ws, L.Wd[i]), dhT, dh0, (int)rows, K, o, H, i > 0};
     hipLaunchKernelGGL(k_sgemm<HeadDxP>, dim3(K / 64 + (K % 64 != 0), (unsigned)((rows + 63) / 64), 1), dim3(256), 0, s,
                        q);
-    HIPCHK(hipMemsetAsync(hd.d_weight, 0, (size_t)K * o * 4, s));
-    HIPCHK(hipMemsetAsync(hd.d_bias, 0, (size_t)o * 4, s));
     HeadDwP w{hT, h0, dZ, P<const float>(ws, L.S[i]), hd.d_weight, K, o, H, rows};
     const unsigned splits = (unsigned)std::max<long>(1, std::min<long>(64, rows / 256));
     hipLaunchKernelGGL(k_sgemm<HeadDwP>, dim3((o + 63) / 64, (K + 63) / 64, splits), dim3(256), 0, s, w);

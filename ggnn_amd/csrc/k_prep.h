@@ -335,3 +335,24 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
   *(uint4*)(ob + (size_t)r * 8) = pk8<F16>(x);
   *(uint4*)(ob + J.lo_off + (size_t)r * 8) = pk8_lo<F16>(x);
 }
+
+// ---- zero the backward's gradient accumulators in one launch (they are
+// accumulated by atomics / per-step adds), instead of one hipMemsetAsync per
+// buffer (each a separate ~5 us fill dispatch).  blockIdx.y = buffer.
+#define ZERO_MAXJ 16
+struct ZeroJobs {
+  float* p[ZERO_MAXJ];
+  long n[ZERO_MAXJ];  // floats
+};
+__global__ void __launch_bounds__(256) k_zero_multi(ZeroJobs a) {
+  float* p = a.p[blockIdx.y];
+  const long n = a.n[blockIdx.y];
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if ((((unsigned long)p) & 15) == 0) {
+    for (; 4 * i + 3 < n; i += stride) *(float4*)(p + 4 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long k = (n & ~3L) + (long)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) p[k] = 0.f;
+  } else {
+    for (; i < n; i += stride) p[i] = 0.f;
+  }
+}
