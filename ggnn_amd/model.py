@@ -243,11 +243,12 @@ class DenseGGNNChemModel(BtbBatching):
         ``*_fixed`` edge weights/biases, as compute_timestep_fast does (:396-412)."""
         if "adjacency_matrix" not in self.placeholders and "adjacency_edges" not in self.placeholders:
             raise RuntimeError("feed() a minibatch before compute_final_node_representations()")
-        if self.args.get("--pr", "btb") not in ("btb",) or self.args.get("--old"):
-            # the identity/--old variants compute the same contraction in another
-            # order; only the btb layout is wired to the engine
-            if self.args.get("--pr", "btb") != "btb":
-                raise NotImplementedError("only --pr btb is supported by the engine")
+        # --old (compute_timestep_normal, :350-389) is the same contraction in
+        # another summation order with element-wise independent edge-weight
+        # dropout, so the engine serves it too (tests: oracle ordering="old");
+        # the identity task is out of scope
+        if self.args.get("--pr", "btb") != "btb":
+            raise NotImplementedError("only --pr btb is supported by the engine")
         T = self.params["num_timesteps"] if fixed_ts is None else int(fixed_ts)
         W = self.weights["edge_weights"] if fixed_ts is None else self.weights["edge_weights_fixed"]
         beta = None

@@ -283,6 +283,31 @@ def test_drop_in_model_on_reference_dev_batches():
         assert _nmax(m.weights["node_gru"]["gates_kernel"].grad.cpu().numpy(), gref["gates_kernel"]) <= FP32_TOL
 
 
+def test_old_ordering_served_by_engine():
+    """--old (compute_timestep_normal, chem_tensorflow_dense.py:350-389) runs
+    through the engine and matches the oracle's per-channel summation order;
+    --pr identity is refused."""
+    torch = _torch()
+    from ggnn_amd.model import DenseGGNNChemModel
+    b, v, h, C, T = 3, 40, 128, 4, 3
+    A, h0 = O.synthetic_batch(b, v, h, C, seed=7, density=0.1)
+    m = DenseGGNNChemModel(args={"--pr": "btb", "--old": True},
+                           params={"hidden_size": h, "num_timesteps": T, "batch_size": b},
+                           num_edge_types=C // 2, precision="fp32", seed=3)
+    w64 = {"edge_weights": m.weights["edge_weights"].detach().cpu().numpy().astype(np.float64),
+           "edge_biases": m.weights["edge_biases"].detach().cpu().numpy().astype(np.float64)}
+    w64.update({k: t.detach().cpu().numpy().astype(np.float64) for k, t in m.weights["node_gru"].items()})
+    m.feed({"adjacency_matrix": A, "num_graphs": b, "num_vertices": v})
+    out = m.compute_final_node_representations(torch.from_numpy(h0).to(m.device))
+    ref, _ = O.forward(A.astype(np.float64), h0.astype(np.float64), w64, T, ordering="old", keep_cache=False)
+    assert np.abs(out.detach().cpu().numpy() - ref).max() <= FP32_TOL
+    m2 = DenseGGNNChemModel(args={"--pr": "identity"}, params={"hidden_size": h, "num_timesteps": T},
+                            num_edge_types=C // 2, precision="fp32", seed=3)
+    m2.feed({"adjacency_matrix": A, "num_graphs": b, "num_vertices": v})
+    with pytest.raises(NotImplementedError):
+        m2.compute_final_node_representations(torch.from_numpy(h0).to(m2.device))
+
+
 # ------------------------------------------------------------------ dropout
 @pytest.mark.parametrize("b,v,h,C,T,t", [(3, 21, 128, 4, 3, 0), (2, 128, 256, 8, 5, 4), (5, 50, 64, 6, 2, 1)])
 def test_dropout_masks_bit_exact(b, v, h, C, T, t):
