@@ -116,7 +116,7 @@ def check(rc: int, what: str) -> None:
         raise GGNNError("%s failed (%d): %s" % (what, rc, msg))
 
 
-def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "bf16",
+def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "fp32",
          edge_keep: float = 1.0, state_keep: float = 1.0, seed: int = 0) -> GGNNDims:
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s" % (PRECISIONS,))

@@ -204,6 +204,8 @@ class BtbBatching:
         bs = self.params["batch_size"]
         keep = self.params.get("graph_state_dropout_keep_prob", 1.0) if is_training else 1.0
         emb_keep = self.params.get("emb_dropout_keep_prob", 1.0) if is_training else 1.0
+        # the output-layer keep is fed 1.0 outside training (run_epoch, chem_tensorflow.py:586-592)
+        out_keep = self.params.get("out_layer_dropout_keep_prob", 1.0) if is_training else 1.0
         for bidx in bucket_at_step:
             elements = bucketed[bidx][counters[bidx] * bs:(counters[bidx] + 1) * bs]
             batch = self.make_batch(elements)
@@ -224,6 +226,7 @@ class BtbBatching:
                 "graph_state_keep_prob": keep,
                 "edge_weight_dropout_keep_prob": keep,
                 "emb_dropout_keep_prob": emb_keep,
+                "out_layer_dropout_keep_prob": out_keep,
                 "sentences_id": batch["sentences_id"],
                 "word_inputs": word_inputs,
                 "target_pos": pad("target_pos"),

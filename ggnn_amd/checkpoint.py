@@ -20,7 +20,10 @@ TF1 graph's naming for the variables this build holds:
   (chem_tensorflow.py:329-341);
 * Adam slots ``<var>/Adam:0`` (m), ``<var>/Adam_1:0`` (v) and
   ``beta1_power:0`` / ``beta2_power:0`` (tf.compat.v1.train.AdamOptimizer,
-  chem_tensorflow.py:494).
+  chem_tensorflow.py:494).  The powers are float32 as in TF, and 0.9**t
+  underflows float32 near t = 1000, so the integer Adam step count is also
+  stored, as the top-level key ``adam_step`` (the reference's restore reads
+  only ``params``/``weights``/``train_step``/``valid_step`` and ignores it).
 
 Parity of the names is unpinned: no TF checkpoint of the reference exists here
 to compare against (TensorFlow is not installed).  Round trips
@@ -95,19 +98,39 @@ def save_progress(model, model_path: str, train_step: int, valid_step: int) -> N
         weights["beta2_power:0"] = np.float32(opt.b2 ** opt.t)
     data = {"params": dict(model.params), "weights": weights, "train_step": int(train_step),
             "valid_step": int(valid_step)}
+    if opt is not None:
+        data["adam_step"] = int(opt.t)
     with open(model_path, "wb") as f:
         pickle.dump(data, f, pickle.HIGHEST_PROTOCOL)
+
+
+def _adam_step_count(data, opt):
+    """Adam's step count t: the stored integer, else recovered from the
+    float32 beta powers (beta2 ** t stays a normal float32 far longer than
+    beta1 ** t, which underflows near t = 1000); None if absent."""
+    if "adam_step" in data:
+        return int(data["adam_step"])
+    saved = data["weights"]
+    for key, beta in (("beta2_power:0", opt.b2), ("beta1_power:0", opt.b1)):
+        p = float(saved.get(key, 0.0))
+        if 0.0 < p < 1.0 and p >= 1.1754944e-38:
+            return int(round(math.log(p) / math.log(beta)))
+    return None
 
 
 def restore_progress(model, model_path: str, log=print):
     """chem_tensorflow.py:816-855: load the pickle, assign every variable the
     file names (shape-checked), keep missing ones as initialised, report
-    unused names.  Adam state is restored when the file holds it and the
-    model has an optimizer.  Returns (train_step, valid_step)."""
+    unused names.  Adam state (slots and step count) is restored when the file
+    holds it, creating the model's optimizer if it has none yet, as the
+    reference's restore fills the Adam slot variables of a fresh graph.
+    Returns (train_step, valid_step)."""
     with open(model_path, "rb") as f:
         data = pickle.load(f)  # the reference's format is a pickle: trusted files only
     saved = data["weights"]
     names = variable_names(model)
+    if getattr(model, "optimizer", None) is None and any(n.endswith("/Adam:0") for n in saved):
+        model.make_optimizer()
     slots, opt = _adam_slots(model, names)
     targets = dict(names)
     targets.update(slots)
@@ -122,9 +145,11 @@ def restore_progress(model, model_path: str, log=print):
                 used.add(n)
             elif n in names:
                 log("Freshly initializing %s since no saved value was found." % n)
-    if opt is not None and "beta1_power:0" in saved:
-        opt.t = int(round(math.log(float(saved["beta1_power:0"])) / math.log(opt.b1)))
-        used.update(("beta1_power:0", "beta2_power:0"))
+    if opt is not None:
+        t = _adam_step_count(data, opt)
+        if t is not None:
+            opt.t = t
+        used.update(n for n in ("beta1_power:0", "beta2_power:0") if n in saved)
     for n in saved:
         if n not in used and not (opt is None and ("/Adam" in n or n.startswith("beta"))):
             log("Saved weights for %s not used by model." % n)

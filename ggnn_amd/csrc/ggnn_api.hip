@@ -176,7 +176,7 @@ AdjL adj_layout(const Cfg& c) {
 struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
-  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp;
+  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp, gmax;
   size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
@@ -213,6 +213,7 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.dMT = o;  o += C * L.nhw * T;
     if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
     L.dbp = o; o += al(T * (size_t)c.b * C * H * 4);    // per-(timestep, graph) dL/dbeta partials
+    L.gmax = o; o += al(4);                               // max |dL/dh_T| (gradient scale, ggnn_common.h)
   }
   L.total = o;
   return L;
@@ -243,10 +244,12 @@ void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, const P
 }
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, const PackL& PL,
-                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp, hipStream_t s) {
+                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp, const uint32_t* gmax,
+                     hipStream_t s) {
   Prof p(K_PROP_BWD, s);
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
-                     P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1);
+                     P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1,
+                     gmax);
 }
 template <int H, int RT, int PREC>
 void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const float* hf, const PackL& PL,
@@ -269,11 +272,11 @@ void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const fl
 template <int H, int RT, int PREC>
 void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
                     const PackL& PL, const void* pk, void* dXT, float* dh_out, void* dzcT, void* dzgT, float* dbc,
-                    float* dbg, hipStream_t s) {
+                    float* dbg, const uint32_t* gmax, hipStream_t s) {
   Prof p(K_GRU_BWD, s);
   hipLaunchKernelGGL((k_gru_bwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, delta, hf, r, u, cc,
                      P<u16>(pk, PL.WcT), P<u16>(pk, PL.WgT), PL.loWc, PL.loWg, (ActT<PREC>*)dXT, dh_out,
-                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N);
+                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N, gmax);
 }
 
 #define DISPATCH_V(c, FN, H, PREC, ...)                 \
@@ -349,7 +352,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H,
                        dense ? (float*)nullptr : hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N,
-                       (int)Prec<PREC>::f16, kNoDrop, 0);
+                       (int)Prec<PREC>::f16, kNoDrop, 0, (const uint32_t*)nullptr);
   }
   if (SPLIT && c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT) {
     // the whole T-step forward of each graph in one workgroup (k_fused.h)
@@ -413,7 +416,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   if (!dense) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, hfin, c.vin, c.V, c.H, hT,
-                       (long)c.b);
+                       (long)c.b, (const uint32_t*)nullptr);
   }
   LAUNCHCHK();
   return GGNN_OK;
@@ -462,6 +465,16 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     z.add(dbc, H);
     if (c.ed) z.add(P<float>(ws, L.G), (long)c.T * c.C * H * H);
     if (use_bias) z.add(dbeta, (long)c.C * H);
+    z.add(P<float>(ws, L.gmax), 1);
+  }
+  // gradient scale: the backward runs on S * dL/dh_T, S = 2^-floor(log2 max|dL/dh_T|),
+  // and divides its outputs by S (ggnn_common.h gscale): loss-normalised
+  // gradients (~1/b) stay inside the f16 limbs' normal range
+  const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
+  {
+    Prof p(K_IO, s);
+    const long n = (long)c.b * c.vin * H;
+    hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(n / 4 + 1), 1024)), dim3(256), 0, s, dhT, n, P<uint32_t>(ws, L.gmax));
   }
   float* dA = P<float>(ws, L.dA);
   float* dB = P<float>(ws, L.dB);
@@ -472,16 +485,20 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   if (!in_place) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
-                       c.sdrop, c.T - 1);
+                       c.sdrop, c.T - 1, gmax);
   }
   for (int t = c.T - 1; t >= 0; --t) {
-    const float* delta = (t == c.T - 1 && in_place) ? dhT : dA;
-    float* dh_out = (t == 0 && dense) ? dh0 : dA;
+    const bool first = t == c.T - 1 && in_place, last = t == 0 && dense;
+    const float* delta = first ? dhT : dA;
+    float* dh_out = last ? dh0 : dA;
     DISPATCH_HRT(c, launch_gru_bwd, PREC, c, delta, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
-                 P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg, s);
+                 P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg,
+                 first ? gmax : (const uint32_t*)nullptr, s);
     DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg), PL, pack,
-                dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t), use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr, s);
+                dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t),
+                use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr,
+                last ? gmax : (const uint32_t*)nullptr, s);
   }
   // all weight gradients in one grouped launch over every timestep (measured:
   // 20 % faster than one launch per timestep right after its producers, whose
@@ -496,10 +513,22 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     Prof p(K_IO, s);
     if (!dense)
       hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
-                         (long)c.b);
+                         (long)c.b, gmax);
     if (use_bias)
       hipLaunchKernelGGL(k_sum_graphs, dim3(grid1d((long)c.C * H, 64), 64), dim3(64), 0, s, P<const float>(ws, L.dbp),
                          dbeta, c.T * c.b, (long)c.C * H);
+    // weight gradients / S
+    ZeroJobs j;
+    memset(&j, 0, sizeof(j));
+    int nj = 0;
+    auto add = [&](float* p, long n) { j.p[nj] = p; j.n[nj++] = n; };
+    add(dW, (long)c.C * H * H);
+    add(dWg, 4 * H * H);
+    add(dbg, 2 * H);
+    add(dWc, 2 * H * H);
+    add(dbc, H);
+    if (use_bias) add(dbeta, (long)c.C * H);
+    hipLaunchKernelGGL(k_unscale_multi, dim3(128, nj), dim3(256), 0, s, j, gmax);
   }
 
   LAUNCHCHK();

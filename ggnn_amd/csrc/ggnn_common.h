@@ -275,6 +275,24 @@ DEV uint4 edge_words(const Drop& d, int c, int i, int j, int t) {
 }
 DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x * d.scale : 0.0f; }
 
+// ---- backward gradient scaling.  The btb loss is divided by the number of
+// targets (chem_tensorflow.py:360,399-403), so dL/dh_T arrives at ~1/b per
+// element; as f16 limbs such values sit at or below the f16 normal range
+// (2^-14) and lose their low bits.  The backward therefore runs on
+// S * dL/dh_T with S = 2^-floor(log2 max|dL/dh_T|) (exact: a power of two,
+// so S*x and x/S are the same fp32 mantissas) and divides every output by S.
+// gmax holds the bit pattern of max|dL/dh_T| (non-negative floats order like
+// their bits, so an atomicMax on the bits is a max on the values).
+DEV int gscale_exp(uint32_t gmax_bits) {
+  const float m = __uint_as_float(gmax_bits);
+  if (!(m > 0.0f) || !(m < 3.0e38f)) return 0;  // zero / non-finite: no scaling
+  int e = ((int)(gmax_bits >> 23) & 0xff) - 127;  // floor(log2 m) for normal m
+  if (e == -127) e = -126;                         // subnormal maxima: scale by 2^126 at most
+  return -max(-126, min(126, e));
+}
+DEV float gscale(const uint32_t* gmax) { return gmax ? __builtin_ldexpf(1.0f, gscale_exp(*gmax)) : 1.0f; }
+DEV float gunscale(const uint32_t* gmax) { return gmax ? __builtin_ldexpf(1.0f, -gscale_exp(*gmax)) : 1.0f; }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // cache-policy operand of the raw buffer builtins: nontemporal (gfx950 NT bit),
 // for write-once streams that are read back only by a later kernel (measured:

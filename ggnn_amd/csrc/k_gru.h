@@ -222,9 +222,10 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
           float* __restrict__ dh_out, u16* __restrict__ dzcT, u16* __restrict__ dzgT,
-          float* __restrict__ dbc, float* __restrict__ dbg, long N) {
+          float* __restrict__ dbc, float* __restrict__ dbg, long N, const uint32_t* __restrict__ gmax) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
+  const float ds = gscale(gmax);  // gradient scale of dL/dh_T read in place (ggnn_common.h), else 1
   typedef Swz<ZCH> SZ;
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = R * 2 * H * 2;
@@ -258,7 +259,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld(pd, vo, so), u = uq[i], c = cq[i], h = bld(ph, vo, so);
+        const float d = bld(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
         du[rt][4 * q + i] = d * u;

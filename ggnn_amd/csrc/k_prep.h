@@ -98,14 +98,15 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
 // the limb format (bf16, or f16 when f16 != 0).  With dr.thr != 0 the state
 // dropout mask of timestep t is applied (backward: dL/dh_T -> dL/dh'_{T-1}).
 __global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H, float* __restrict__ hf,
-                            u16* __restrict__ hb, long N, int f16, Drop dr, int t) {
+                            u16* __restrict__ hb, long N, int f16, Drop dr, int t, const uint32_t* gmax) {
   const long total = N * H;
+  const float sc = gscale(gmax);  // backward staging of dL/dh_T: the gradient scale (ggnn_common.h)
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const long row = q / H;
     const int col = q % H;
     const long g = row / V;
     const int i = row % V;
-    float x = (i < vin) ? h0[(g * vin + i) * H + col] : 0.0f;
+    float x = (i < vin) ? h0[(g * vin + i) * H + col] * sc : 0.0f;
     if (dr.thr) x = drop_apply(dr, u4_get(state_words(dr, (int)g, i, col, t), i & 3), x);
     if (hf) hf[q] = x;
     if (hb) hb[q] = f16 ? to_limb<true>(x) : to_limb<false>(x);
@@ -113,14 +114,16 @@ __global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H,
 }
 
 // hf [N][H] fp32 -> out [b][vin][H]
-__global__ void k_unpad_state(const float* __restrict__ hf, int vin, int V, int H, float* __restrict__ out, long b) {
+__global__ void k_unpad_state(const float* __restrict__ hf, int vin, int V, int H, float* __restrict__ out, long b,
+                              const uint32_t* gmax) {
   const long total = b * vin * (long)H;
+  const float sc = gunscale(gmax);  // backward: undo the gradient scale
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const long r = q / H;
     const int col = q % H;
     const long g = r / vin;
     const int i = r % vin;
-    out[q] = hf[(g * V + i) * H + col];
+    out[q] = hf[(g * V + i) * H + col] * sc;
   }
 }
 
@@ -355,4 +358,41 @@ __global__ void __launch_bounds__(256) k_zero_multi(ZeroJobs a) {
   } else {
     for (; i < n; i += stride) p[i] = 0.f;
   }
+}
+
+// ---- max |x| over n floats into *gmax (as bits; *gmax zeroed beforehand):
+// the backward's gradient scale (gscale, ggnn_common.h)
+__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, long n, uint32_t* __restrict__ gmax) {
+  float m = 0.0f;
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if ((((unsigned long)x) & 15) == 0) {
+    for (; 4 * i + 3 < n; i += stride) {
+      const float4 a = *(const float4*)(x + 4 * i);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+    }
+    for (long k = (n & ~3L) + (long)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) m = fmaxf(m, fabsf(x[k]));
+  } else {
+    for (; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  }
+  // (fmaxf drops NaN; an inf stays inf and disables the scaling)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    atomicMax(gmax, __float_as_uint(m));
+  }
+}
+
+// ---- divide the backward's outputs by the gradient scale (grouped like
+// k_zero_multi; blockIdx.y = buffer)
+__global__ void __launch_bounds__(256) k_unscale_multi(ZeroJobs a, const uint32_t* __restrict__ gmax) {
+  float* p = a.p[blockIdx.y];
+  const long n = a.n[blockIdx.y];
+  const float sc = gunscale(gmax);
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] *= sc;
 }

@@ -143,7 +143,8 @@ template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
            const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
-           u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm) {
+           u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
+           const uint32_t* __restrict__ gmax) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
@@ -278,12 +279,13 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
   // dL/dh_t -> dL/dh'_{t-1} through the state dropout of timestep tm = t-1
   const bool drop = dr.thr != 0 && tm >= 0;
+  const float osc = gunscale(gmax);  // last step writing dL/dh0 in place: undo the gradient scale, else 1
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt) {
     uint4 dw = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float x = adh[jt][r];
+      float x = adh[jt][r] * osc;
       if (drop) {
         if ((r & 3) == 0) dw = state_words(dr, g, jt * 32 + acc_row0(r) + 4 * hh, n, tm);
         x = drop_apply(dr, u4_get(dw, r & 3), x);

@@ -58,9 +58,11 @@ class PropagationEngine:
     and its backward for batches of shape [b, C, v, v] / [b, v, h]."""
 
     def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None,
-                 precision: str = "bf16"):
-        """precision: "bf16" (bf16 MFMA operands, fp32 accumulation) or "fp32"
-        (GGNN_FP32_PARITY: split-bf16 operands, matches fp32 to <= 1e-3)."""
+                 precision: str = "fp32"):
+        """precision: "fp32" (GGNN_FP32_PARITY, the default: every non-exact MFMA
+        operand of the propagation as an f16 hi/lo limb pair, fp32 accumulation,
+        matches the reference's fp32 math to <= 1e-3), "fp16" or "bf16" (single
+        16-bit MFMA operands, fp32 accumulation; reduced precision, opt-in)."""
         self.h = int(hidden)
         self.C = int(channels)
         self.use_edge_bias = bool(use_edge_bias)

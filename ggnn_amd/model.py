@@ -92,7 +92,7 @@ class DenseGGNNChemModel(BtbBatching):
     """Hot-path subset of the reference's DenseGGNNChemModel (btb task)."""
 
     def __init__(self, args=None, params=None, num_edge_types=None, output_size_edges=12, pos_size=46,
-                 bucket_max_nodes=120, device=None, seed=None, precision="bf16", vocab_size=1000, max_nodes=None,
+                 bucket_max_nodes=120, device=None, seed=None, precision="fp32", vocab_size=1000, max_nodes=None,
                  embedding_sizes=None):
         self.args = dict(args or {"--pr": "btb"})
         self.params = self.default_params()
@@ -250,10 +250,14 @@ class DenseGGNNChemModel(BtbBatching):
         if self.args.get("--pr", "btb") != "btb":
             raise NotImplementedError("only --pr btb is supported by the engine")
         T = self.params["num_timesteps"] if fixed_ts is None else int(fixed_ts)
-        W = self.weights["edge_weights"] if fixed_ts is None else self.weights["edge_weights_fixed"]
+        # compute_timestep_fast picks the *_fixed twins when fixed_ts is given
+        # (:396-412); compute_timestep_normal (--old, :350-389) always uses the
+        # main edge_weights / edge_biases
+        fixed = fixed_ts is not None and not self.args.get("--old")
+        W = self.weights["edge_weights_fixed"] if fixed else self.weights["edge_weights"]
         beta = None
         if self.params["use_edge_bias"]:
-            beta = self.weights["edge_biases"] if fixed_ts is None else self.weights["edge_biases_fixed"]
+            beta = self.weights["edge_biases_fixed"] if fixed else self.weights["edge_biases"]
         h0 = initial_node_representations
         if not isinstance(h0, torch.Tensor):
             h0 = torch.from_numpy(np.ascontiguousarray(np.asarray(h0, dtype=np.float32)))
@@ -351,11 +355,17 @@ class DenseGGNNChemModel(BtbBatching):
         if all_reduce is not None:
             all_reduce(grads)
         if self.optimizer is None:
-            self.optimizer = ClipAdam(params, learning_rate=self.params["learning_rate"],
-                                      clamp_gradient_norm=self.params["clamp_gradient_norm"])
+            self.make_optimizer()
         sq = [self.lookup_sqnorm.get(id(p)) for p in params]
         self.optimizer.step(grads, grad_scale=grad_scale, sqnorms=sq)
         return loss
+
+    def make_optimizer(self) -> ClipAdam:
+        """The reference's train step optimizer (chem_tensorflow.py:494-503) over
+        ``trainable_variables()``: clip_by_norm(clamp_gradient_norm) + Adam."""
+        self.optimizer = ClipAdam(self.trainable_variables(), learning_rate=self.params["learning_rate"],
+                                  clamp_gradient_norm=self.params["clamp_gradient_norm"])
+        return self.optimizer
 
     # ------------------------------------------------- checkpoint / evaluation
     def save_progress(self, model_path: str, train_step: int, valid_step: int) -> None:

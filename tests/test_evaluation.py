@@ -100,7 +100,8 @@ def test_checkpoint_round_trip(tmp_path):
     a.save_progress(path, train_step=11, valid_step=4)
     with open(path, "rb") as f:
         data = pickle.load(f)  # our own file
-    assert set(data) == {"params", "weights", "train_step", "valid_step"}
+    # the reference's four keys (chem_tensorflow.py:800-806) plus the integer Adam step
+    assert set(data) == {"params", "weights", "train_step", "valid_step", "adam_step"}
     assert data["params"]["hidden_size"] == 64
     assert "graph_model/Variable/Adam:0" in data["weights"] and "beta1_power:0" in data["weights"]
     logs = []
@@ -133,3 +134,16 @@ def test_checkpoint_restore_tolerates_missing_and_reports_unused(tmp_path):
         pickle.dump(data, f)
     with pytest.raises(ValueError):
         K.restore_progress(b, path, log=logs.append)
+
+
+def test_adam_step_count_survives_float32_underflow():
+    """checkpoint._adam_step_count: the stored integer wins; without it the
+    float32 beta2 power (0.999**t) recovers t long after 0.9**t has underflowed."""
+    from types import SimpleNamespace
+    from ggnn_amd.checkpoint import _adam_step_count
+    opt = SimpleNamespace(b1=0.9, b2=0.999)
+    for t in (1, 25, 983, 1000, 5000, 40000):
+        w = {"beta1_power:0": np.float32(0.9 ** t), "beta2_power:0": np.float32(0.999 ** t)}
+        assert _adam_step_count({"weights": w}, opt) == t, t
+        assert _adam_step_count({"weights": w, "adam_step": t}, opt) == t
+    assert _adam_step_count({"weights": {}}, opt) is None

@@ -97,34 +97,38 @@ def test_heads_forward_backward_parity(b, v, h, os_, keep):
     assert _nmax(dh0.cpu().numpy(), rh0) <= 1e-5
 
 
-def _dev_model(torch, keep_all):
+def _dev_model(torch, keep_all, hidden=128, batch_size=6, emb=None, big_batch=False):
     from ggnn_amd.model import DenseGGNNChemModel
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
     data = json.loads(str(g["raw_json"]))
     vocab = 1 + max(max(d["words_index"]) for d in data)
-    params = {"hidden_size": 128, "num_timesteps": 2, "batch_size": 6, "learning_rate": 0.003}
+    params = {"hidden_size": hidden, "num_timesteps": 2, "batch_size": batch_size, "learning_rate": 0.003}
     if keep_all:
         params.update(graph_state_dropout_keep_prob=1.0, emb_dropout_keep_prob=1.0, out_layer_dropout_keep_prob=1.0)
     m = DenseGGNNChemModel(params=params, num_edge_types=int(g["num_edge_types"]),
                            output_size_edges=int(g["output_size_edges"]), pos_size=int(g["pos_size"]),
                            bucket_max_nodes=int(g["bucket_max_nodes"]), precision="fp32", vocab_size=vocab,
-                           embedding_sizes=dict(loc=16, pos=8, word=16, edge=8))
+                           embedding_sizes=emb or dict(loc=16, pos=8, word=16, edge=8))
+    if big_batch:
+        # one full batch of real dev sentences: the sentences of the most
+        # populated bucket, repeated until batch_size graphs share that bucket
+        sizes = m.get_bucket_sizes()
+        bucket = [int(np.argmax(sizes > max(max(e[0], e[2]) for e in d["graph"]))) for d in data]
+        top = max(set(bucket), key=bucket.count)
+        pool = [d for d, k in zip(data, bucket) if k == top]
+        data = [pool[i % len(pool)] for i in range(batch_size)]
+        feeds = list(m.make_minibatch_iterator(m.process_raw_graphs(data, True), True))
+        assert feeds[0]["num_graphs"] == batch_size
+        return m, feeds
     feeds = list(m.make_minibatch_iterator(m.process_raw_graphs(data[:30], True), True))
     return m, feeds
 
 
-@pytest.mark.parametrize("dropout", [False, True])
-def test_model_train_step_matches_oracle(dropout):
-    """One whole btb training step of the drop-in model on real dev batches
-    (front-end -> propagation -> heads -> loss -> backward -> clip + Adam)
-    against the oracle composed the same way, including the IndexedSlices
-    clip norm of the embeddings and every dropout mask (replayed from the
-    seeds the model drew)."""
-    torch = _torch()
-    m, feeds = _dev_model(torch, keep_all=not dropout)
-    fd = feeds[0]
-    if dropout:
-        fd = dict(fd, edge_weight_dropout_keep_prob=0.9, graph_state_keep_prob=0.9)
+def _check_train_step(m, fd):
+    """One whole btb training step of the drop-in model against the oracle
+    composed the same way, including the IndexedSlices clip norm of the
+    embeddings and every dropout mask (replayed from the seeds the model
+    drew)."""
     params = m.trainable_variables()
     before = [p.detach().cpu().numpy().astype(np.float64) for p in params]
     loss = m.train_step(fd)
@@ -166,7 +170,7 @@ def test_model_train_step_matches_oracle(dropout):
     lr, clip = m.params["learning_rate"], m.params["clamp_gradient_norm"]
     lr_t = lr * np.sqrt(1 - 0.999) / (1 - 0.9)
     for i, (p0, g) in enumerate(zip(before, grads)):
-        assert _nmax(params[i].grad.cpu().numpy(), g) <= TOL, i
+        assert _nmax(params[i].grad.cpu().numpy(), g) <= TOL, (i, _nmax(params[i].grad.cpu().numpy(), g))
         if sqn[i] is not None:
             got = m.lookup_sqnorm[id(params[i])]
             assert abs(float(got) - sqn[i]) <= 1e-4 * sqn[i], i
@@ -179,6 +183,34 @@ def test_model_train_step_matches_oracle(dropout):
         sig = np.abs(gc) > 1e-3 * max(np.abs(gc).max(), 1e-30)
         assert np.abs(after[i] - ref)[sig].max(initial=0.0) <= lr * 1e-2, i
         assert np.abs(after[i] - ref).max() <= 2.01 * lr, i
+    return gp
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_model_train_step_matches_oracle(dropout):
+    """One whole btb training step of the drop-in model on real dev batches
+    (front-end -> propagation -> heads -> loss -> backward -> clip + Adam)
+    against the oracle."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=not dropout)
+    fd = feeds[0]
+    if dropout:
+        fd = dict(fd, edge_weight_dropout_keep_prob=0.9, graph_state_keep_prob=0.9)
+    _check_train_step(m, fd)
+
+
+def test_model_train_step_full_batch_hidden256():
+    """The same whole training step at a real batch size: 64 WSJ dev graphs in
+    one bucket, hidden 256, C = 92 channels, the training feed's dropouts.  The
+    loss is divided by ~64 * n targets, so dL/dh_T is at the btb loss's real
+    magnitude (chem_tensorflow.py:360,399-403), where the backward's gradient
+    scale matters."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=False, hidden=256, batch_size=64,
+                          emb=dict(loc=64, pos=32, word=96, edge=32), big_batch=True)
+    fd = feeds[0]
+    gp = _check_train_step(m, fd)
+    assert np.abs(gp["h0"]).max() < 2.0 ** -5   # at the loss scale (~1/b), not O(1)
 
 
 def test_model_trains_on_dev_batches():
@@ -209,11 +241,27 @@ def test_evaluate_batch_las_uas_and_checkpoint_resume(tmp_path):
     assert uas1 > uas0 and las1 >= las0
     path = str(tmp_path / "model.pickle")
     m.save_progress(path, train_step=25, valid_step=0)
-    m2, _ = _dev_model(torch, keep_all=True)
-    m2.feed(fd)
-    m2.train_step(fd)  # creates the optimizer state that the restore overwrites
+    m2, _ = _dev_model(torch, keep_all=True)   # fresh model: no optimizer yet, restore creates it
+    assert m2.optimizer is None
     assert m2.restore_progress(path) == (25, 0)
+    assert m2.optimizer is not None and m2.optimizer.t == m.optimizer.t == 25
     for _ in range(2):  # the second loss sees one Adam update from the restored state
         l_a = float(m.train_step(fd).detach())
         l_b = float(m2.train_step(fd).detach())
         assert abs(l_a - l_b) <= 1e-5 * max(1.0, abs(l_a))
+
+
+def test_checkpoint_restores_adam_step_past_float32_underflow(tmp_path):
+    """beta1_power = 0.9**t underflows float32 near t = 1000; the Adam step
+    count must survive a save/restore well past it (checkpoint.py)."""
+    torch = _torch()
+    m, feeds = _dev_model(torch, keep_all=True)
+    m.train_step(feeds[0])
+    m.optimizer.t = 4321
+    path = str(tmp_path / "late.pickle")
+    m.save_progress(path, train_step=4321, valid_step=7)
+    m2, _ = _dev_model(torch, keep_all=True)
+    assert m2.restore_progress(path) == (4321, 7)
+    assert m2.optimizer.t == 4321
+    for a, b in zip(m.optimizer.m, m2.optimizer.m):
+        assert torch.equal(a, b)
