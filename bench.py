@@ -77,52 +77,65 @@ def kernel_issued_flops(kind, b, v, h, C, T, precision):
     return kernel_algo_flops(kind, b, v, h, C, T)
 
 
-def cpu_baseline(seconds=10.0, sample_b=8):
+def cpu_baseline(reps=5):
     """The oracle (numpy fp32 + OpenBLAS restatement of the reference math) on
-    the host: forward + explicit backward of the same config on `sample_b`
-    graphs, repeated for ~`seconds`."""
+    the host, SURVEY.md §8d: config 3 (fwd+bwd, the bench's workload) and
+    config 2 (fwd only, its parity config), each the median of `reps` timed
+    repetitions after one warm-up, on every core this process may use and on
+    one core.  The thread count is the process's CPU affinity set, capped at
+    OMP_NUM_THREADS (the box's CPU share for one GPU; the box's `nproc` counts
+    the whole host, which other jobs share)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ggnn_oracle as O
     try:
         from threadpoolctl import threadpool_limits
     except Exception:  # pragma: no cover
         threadpool_limits = None
-    cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    C = 2 * CFG["e"]
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        affinity = nproc
+    omp = os.environ.get("OMP_NUM_THREADS")
+    cores = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
 
-    def run(threads, secs, gb):
-        A, h0 = O.synthetic_batch(gb, CFG["v"], CFG["h"], C, seed=1)
-        w = O.synthetic_weights(CFG["h"], C, seed=1, parity_bias=False)
+    def run(threads, cfg, gb, backward):
+        b_, v, h, C, T = gb, cfg["v"], cfg["h"], 2 * cfg["e"], cfg["T"]
+        A, h0 = O.synthetic_batch(b_, v, h, C, seed=1)
+        w = O.synthetic_weights(h, C, seed=1, parity_bias=False)
         dhT = np.ones_like(h0)
         ctx = threadpool_limits(limits=threads) if threadpool_limits else None
         try:
-            n = 0
-            t0 = time.perf_counter()
-            while True:
-                hT, caches = O.forward(A, h0, w, CFG["T"])
-                O.backward(A, dhT, caches, w)
-                n += gb
-                el = time.perf_counter() - t0
-                if el >= secs:
-                    break
+            times = []
+            for i in range(reps + 1):  # one warm-up, then `reps` timed
+                t0 = time.perf_counter()
+                hT, caches = O.forward(A, h0, w, T)
+                if backward:
+                    O.backward(A, dhT, caches, w)
+                if i:
+                    times.append(time.perf_counter() - t0)
         finally:
             if ctx is not None and hasattr(ctx, "restore_original_limits"):
                 ctx.restore_original_limits()
-        return n / el, "oracle fp32 numpy fwd+bwd, %d graphs/batch (v=%d h=%d C=%d T=%d), %d graphs in %.1f s" % (
-            gb, CFG["v"], CFG["h"], C, CFG["T"], n, el)
+        med = float(np.median(times))
+        return dict(value=gb / med, unit="graphs/s", cores=threads,
+                    sample="oracle fp32 numpy %s, %d-graph batch (v=%d h=%d C=%d T=%d), median of %d after 1 warm-up "
+                           "(%.3f s per batch)" % ("fwd+bwd" if backward else "fwd", gb, v, h, C, T, reps, med))
 
-    value, sample = run(cores, seconds, sample_b)
-    # SURVEY §8d: all cores and one core, CPU model stated (the 1-core leg is a
-    # short sample of 2-graph batches so the default bench stays within minutes)
-    v1, s1 = run(1, max(2.0, seconds / 3), 2)
+    c3 = dict(CFG)
+    c2 = dict(b=32, v=64, h=128, e=2, T=3)
+    main_leg = run(cores, c3, 64, True)
     model = None
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
     except OSError:
         pass
-    return dict(value=value, unit="graphs/s", cores=cores, kind="port", sample=sample, cpu_model=model,
-                single_core=dict(value=v1, unit="graphs/s", cores=1, sample=s1))
+    return dict(main_leg, kind="port", cpu_model=model, nproc=nproc, affinity_cpus=affinity,
+                omp_num_threads=omp,
+                single_core=run(1, c3, 4, True),
+                config2_fwd=run(cores, c2, c2["b"], False),
+                config2_fwd_single_core=run(1, c2, c2["b"], False))
 
 
 def adjacency_feed_costs(eng, b, v, E, dev, reps=5):
@@ -246,12 +259,22 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10)
             step()
         torch.cuda.synchronize()
     fr = {}
+    tr = load_traffic(precision) or {}
     for k in ("fwd_fused", "prop_fwd", "prop_bwd", "gru_fwd", "gru_bwd", "wgrad"):
         if timer.launches.get(k):
             avg = timer.total_ms[k] / timer.launches[k]
             fl = kernel_algo_flops(k, b, v, h, C, T)
-            fr[k] = {"avg_launch_ms": avg, "tflops": fl / (avg * 1e-3) / 1e12,
-                     "frac_of_bf16_peak": fl / (avg * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+            d = {"avg_launch_ms": avg, "tflops": fl / (avg * 1e-3) / 1e12,
+                 "frac_of_bf16_peak": fl / (avg * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+            kt = tr.get("kernels", {}).get(k)
+            if kt:
+                # PMC HBM bytes per launch (profiles/pmc_traffic_<precision>.json);
+                # a kernel's roofline fraction is max(F/P_mfma, B/P_hbm)
+                gbs = kt["hbm_bytes_per_launch"] / (avg * 1e-3) / 1e9
+                d.update(traffic=kt["hbm_bytes_per_launch"], hbm_gbs=gbs, frac_of_hbm_peak=gbs / HBM_PEAK_GBS,
+                         frac_roofline=max(d["frac_of_bf16_peak"], gbs / HBM_PEAK_GBS),
+                         traffic_source="profiles/pmc_traffic_%s.json" % precision)
+            fr[k] = d
     return {"precision": precision, "value": b / (ms * 1e-3), "unit": "graphs/s", "ms_per_step": ms,
             "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
 
@@ -266,9 +289,11 @@ def load_ceilings():
         return None
 
 
-def load_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_traffic(precision="fp32"):
+    """Per-launch HBM bytes per kernel kind from the committed PMC summary of
+    this precision mode (tools/pmc_profile.sh)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json" if precision == "fp32" else
+                     "pmc_traffic_%s.json" % precision)
     if os.path.exists(p):
         try:
             with open(p) as f:
@@ -281,12 +306,12 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dropout-keep", type=float, default=0.9,
                     help="keep probability of the dropout-on line (graph_state_dropout_keep_prob)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side measurements (front-end/heads, bf16 mode)")
     ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
@@ -391,12 +416,17 @@ def main():
     fl = kernel_algo_flops(dom, b, v, h, C, T)
     achieved = fl / (avg_ms * 1e-3) / 1e12 if fl else None
     traffic = None
-    tr = load_traffic()
+    tr = load_traffic(args.precision)
+    traffic_src = None
     if tr and tr.get("precision", "fp32") == args.precision and dom in tr.get("kernels", {}):
         traffic = tr["kernels"][dom]["hbm_bytes_per_launch"]
+        traffic_src = ("profiles/pmc_traffic.json (%s): rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                       "collected in separate passes of this bench's command (PMC passes cannot run inside "
+                       "the timed process)" % tr.get("run", "?"))
     roof = {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": (achieved / BF16_DENSE_PEAK_TFLOPS) if achieved else None,
-            "traffic": traffic, "avg_launch_ms": avg_ms, "algo_flops_per_launch": fl}
+            "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": avg_ms,
+            "algo_flops_per_launch": fl}
     ceil = load_ceilings()
     if ceil:
         # library ceilings measured on an MI355X box (tools/ceilings.py): the
@@ -436,8 +466,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": {"fp32": "fp32", "fp16": "fp16", "bf16": "bf16"}[args.precision],
-            "precision_note": {"fp32": "fp32-class: every non-exact MFMA operand as an f16 hi/lo limb pair "
-                                       "(3 products), fp32 accumulation; parity <= 1e-3 vs the fp32 reference",
+            "precision_note": {"fp32": "fp32-class: every non-exact MFMA operand of the forward and of the "
+                                       "dh/dX chain as an f16 hi/lo limb pair (3 products), fp32 accumulation; "
+                                       "the weight-gradient GEMMs (k_wgrad256) take SINGLE f16 operands, on a "
+                                       "power-of-two-scaled gradient; parity <= 1e-3 vs the fp32 reference "
+                                       "(tests/test_gpu_parity.py, incl. loss-scale gradients)",
                                "fp16": "f16 MFMA operands, fp32 accumulation (reduced precision)",
                                "bf16": "bf16 MFMA operands, fp32 accumulation (reduced precision)"}[args.precision],
             "data": "synthetic (SURVEY §8d generator: Bernoulli(0.1) adjacency on n~U{v/2..v} active nodes, glorot weights)",
@@ -456,7 +489,7 @@ def main():
             "bf16_mode": bf16,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         print(json.dumps(res), flush=True)
     if world > 1:
         tdist.destroy_process_group()

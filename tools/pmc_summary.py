@@ -59,6 +59,7 @@ if len(sys.argv) > 2:
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, mean per dispatch; "
                          "FETCH_SIZE doubled (gfx950 correction, MI355X_MICROARCH.md HBM section)",
                "bench_args": os.environ.get("PMC_BENCH_ARGS", ""),
+               "run": os.environ.get("PMC_RUN", ""),
                "precision": (re.findall(r"--precision[= ](\w+)", os.environ.get("PMC_BENCH_ARGS", "")) or ["fp32"])[-1],
                "kernels": kinds},
               open(sys.argv[2], "w"), indent=1, sort_keys=True)
