@@ -279,6 +279,54 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10)
             "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
 
 
+def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
+    """Side measurement (SURVEY §8f rank 3 / configs[4] shapes): the fwd+bwd
+    step on dependency-tree graphs with the real btb label set (std->nivre,
+    E = 46 -> C = 92 channels, most of them empty per graph), with empty-channel
+    skipping on (the default) and off (GGNN_DENSE_CHANNELS).  Sentence-sized
+    graphs (the real dev set: mean 24.6 nodes; bucket v <= 32),
+    n ~ U{v/2..v} nodes, random heads before dependents, Zipf-like labels
+    (P(label k) ~ 1/k: a few labels such as punct/nsubj/det dominate a treebank)."""
+    import torch
+    from ggnn_amd.dist import FlatGradients
+    from ggnn_amd.engine import PropagationEngine
+    import ggnn_oracle as O
+    rng = np.random.default_rng(13)
+    C = 2 * E
+    pz = 1.0 / np.arange(1, E + 1)
+    pz /= pz.sum()
+    graphs = []
+    for _ in range(b):
+        n = int(rng.integers(v // 2, v + 1))
+        graphs.append([(int(rng.integers(0, i)), int(rng.choice(E, p=pz)) + 1, i) for i in range(1, n)])
+    occ = [int((O.graph_to_adj_mat_bd(g_, v, E, dtype=np.float32).reshape(C, -1).max(1) > 0).sum()) for g_ in graphs[:16]]
+    w = O.synthetic_weights(h, C, seed=3)
+    w_d = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
+    h0 = torch.from_numpy(rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)).to(dev)
+    dhT = torch.from_numpy(rng.standard_normal((b, v, h)).astype(np.float32)).to(dev)
+    res = {"workload": "b=%d dependency trees, v=%d, hidden=%d, E=%d (C=%d), T=%d, fwd+bwd" % (
+        b, v, h, E, C, T), "nonempty_channels_per_graph_mean": float(np.mean(occ))}
+    for skip in (True, False):
+        eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision="fp32", skip_empty_channels=skip)
+        eng.set_adjacency_edges(graphs, v, E)
+        grads = FlatGradients(h, C, True, device=dev)
+        gv = dict(grads.views)
+        gv["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+        out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
+
+        def step():
+            pack = eng.pack_weights(w_d, T=T)
+            eng.forward(h0, pack, T, training=True, out=out)
+            eng.backward(dhT, gv)
+
+        ms = _timed_events(step, steps)
+        res["skip" if skip else "dense"] = {"ms_per_step": ms, "graphs_per_s": b / (ms * 1e-3)}
+        del eng, grads, gv, out
+        torch.cuda.empty_cache()
+    res["speedup"] = res["dense"]["ms_per_step"] / res["skip"]["ms_per_step"]
+    return res
+
+
 def load_ceilings():
     """Library MFMA / copy ceilings measured on the box (tools/ceilings.py)."""
     p = os.path.join(ROOT, "profiles", "ceilings.json")
@@ -450,6 +498,7 @@ def main():
     callers = callers_side(dev, b, v, h) if rank == 0 and not args.no_side else None
     bf16 = (precision_side(dev, "bf16", A_d, h0_d, w_d, dhT, b, v, h, C, T)
             if rank == 0 and not args.no_side and args.precision != "bf16" else None)
+    real = real_density_side(dev) if rank == 0 and not args.no_side else None
 
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]
@@ -487,6 +536,7 @@ def main():
                                    "value above is dropout off (keep 1, the parity setting)"},
             "callers": callers,
             "bf16_mode": bf16,
+            "real_density_c92": real,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_reps)

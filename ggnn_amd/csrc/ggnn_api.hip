@@ -105,7 +105,9 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
     return fail(GGNN_EUNSUP, "hidden size must be 64, 128 or 256 (got " + std::to_string(d->h) + ")");
   const int V = pad_v(d->v);
   if (V < 0) return fail(GGNN_EUNSUP, "v must be <= 128 (got " + std::to_string(d->v) + ")");
-  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16)) return fail(GGNN_EINVAL, "unknown flag bits");
+  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS))
+    return fail(GGNN_EINVAL, "unknown flag bits");
+  if (d->C > CHL_MAXC) return fail(GGNN_EUNSUP, "C must be <= " + std::to_string(CHL_MAXC));
   if ((d->flags & GGNN_FP32_PARITY) && (d->flags & GGNN_FP16))
     return fail(GGNN_EINVAL, "GGNN_FP32_PARITY and GGNN_FP16 are exclusive");
   c->b = d->b; c->vin = d->v; c->V = V; c->H = d->h; c->C = d->C; c->T = d->T; c->flags = d->flags;
@@ -160,7 +162,7 @@ PackL pack_layout(const Cfg& c) {
 
 // ---- staged adjacency
 struct AdjL {
-  size_t Ab, AbT, deg, total;
+  size_t Ab, AbT, deg, chl, chl_all, total;
 };
 AdjL adj_layout(const Cfg& c) {
   AdjL L;
@@ -168,6 +170,8 @@ AdjL adj_layout(const Cfg& c) {
   L.Ab = o;  o += al((size_t)c.b * c.C * c.V * c.V * 2);
   L.AbT = o; o += al((size_t)c.b * c.C * c.V * c.V * 2);
   L.deg = o; o += al((size_t)c.b * c.C * c.V * 2);
+  L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);  // per-graph non-empty channel lists (k_chan_list)
+  L.chl_all = o; o += al((size_t)(c.C + 1) * 4);     // identity list (dense channel loop)
   L.total = o;
   return L;
 }
@@ -221,6 +225,17 @@ WsL ws_layout(const Cfg& c, bool training) {
 
 template <typename T> T* P(void* base, size_t off) { return (T*)((char*)base + off); }
 template <typename T> const T* P(const void* base, size_t off) { return (const T*)((const char*)base + off); }
+// the channel list the compute kernels loop over: per-graph non-empty
+// channels (graph stride C+1), or the identity list (stride 0) under
+// GGNN_DENSE_CHANNELS
+struct ChanL {
+  const int* p;
+  int stride;
+};
+ChanL chan_lists(const Cfg& c, const void* adj, const AdjL& AL) {
+  if (c.flags & GGNN_DENSE_CHANNELS) return ChanL{P<int>(adj, AL.chl_all), 0};
+  return ChanL{P<int>(adj, AL.chl), c.C + 1};
+}
 int grid1d(long n, int bs = 256) {
   const long g = (n + bs - 1) / bs;
   return (int)std::min<long>(std::max<long>(g, 1), 8192);
@@ -236,18 +251,19 @@ int gru_rt(const Cfg& c, int maxrt) {
 }
 
 template <int V, int H, int PREC>
-void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, const PackL& PL, const void* pk, void* Xa,
-                     void* XT, hipStream_t s) {
+void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, ChanL chl, const PackL& PL,
+                     const void* pk, void* Xa, void* XT, hipStream_t s) {
   Prof p(K_PROP_FWD, s);
-  hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab,
+  hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab, chl.p, chl.stride,
                      P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
 template <int V, int H, int PREC>
-void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, const PackL& PL,
-                     const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp, const uint32_t* gmax,
-                     hipStream_t s) {
+void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, ChanL chl,
+                     const PackL& PL, const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp,
+                     const uint32_t* gmax, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
-  hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg,
+  hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg, chl.p,
+                     chl.stride,
                      P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1,
                      gmax);
 }
@@ -359,6 +375,9 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     FusedFwdArgs fa;
     memset(&fa, 0, sizeof(fa));
     fa.Ab = P<u16>(adj, AL.Ab);
+    const ChanL cl = chan_lists(c, adj, AL);
+    fa.chl = cl.p;
+    fa.chs = cl.stride;
     fa.Wp = P<u16>(pack, PL.wf(0));
     fa.wlo = PL.loW;
     fa.wstep = c.ed ? (long)(PL.szW / 2) : 0;
@@ -403,7 +422,8 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     u16* hb_out = SPLIT ? nullptr : P<u16>(ws, L.hb[(t + 1) & 1]);
     const void* hs = SPLIT ? (const void*)hf_in : (const void*)hb_in;
     void* XT = tr ? P<void>(ws, L.XT + L.nhw * t) : nullptr;
-    DISPATCH_VH(c, launch_prop_fwd, PREC, c, t, hs, P<u16>(adj, AL.Ab), PL, pack, P<void>(ws, L.Xa), XT, s);
+    DISPATCH_VH(c, launch_prop_fwd, PREC, c, t, hs, P<u16>(adj, AL.Ab), chan_lists(c, adj, AL), PL, pack,
+                P<void>(ws, L.Xa), XT, s);
     void* hTo = (tr && t + 1 < c.T) ? P<void>(ws, L.hT + L.nhw * (t + 1)) : nullptr;
     float* ro = tr ? P<float>(ws, L.r + L.nh4 * t) : nullptr;
     float* uo = tr ? P<float>(ws, L.u + L.nh4 * t) : nullptr;
@@ -495,7 +515,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg,
                  first ? gmax : (const uint32_t*)nullptr, s);
-    DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg), PL, pack,
+    DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg),
+                chan_lists(c, adj, AL), PL, pack,
                 dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t),
                 use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr,
                 last ? gmax : (const uint32_t*)nullptr, s);
@@ -825,6 +846,8 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
                          c.vin, num_edge_types, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT));                           \
     hipLaunchKernelGGL((k_adj_deg<VV, F>), dim3((unsigned)tiles), dim3(VV), 0, s, P<const u16>(adj, L.Ab),        \
                        P<u16>(adj, L.deg));                                                                      \
+    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,               \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                              \
   } while (0)
   const bool f16 = c.prec != PREC_BF16;
   if (c.V == 32) { if (f16) ADJ_EDGES(32, true); else ADJ_EDGES(32, false); }
@@ -845,8 +868,12 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
   const dim3 grid((unsigned)(c.b * c.C));
   Prof p(K_ADJ, s);
 #define PREP_ADJ(VV, F)                                                                                       \
-  hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT), \
-                     P<u16>(adj, L.deg))
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab),                 \
+                       P<u16>(adj, L.AbT), P<u16>(adj, L.deg));                                               \
+    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,             \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                           \
+  } while (0)
   if (c.prec != PREC_BF16) {
     if (c.V == 32) PREP_ADJ(32, true);
     else if (c.V == 64) PREP_ADJ(64, true);

@@ -290,6 +290,42 @@ __global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, u16* 
   deg[tile * V + threadIdx.x] = to_limb<F16>(s);
 }
 
+// ---- per-graph list of non-empty channels (about 60 % of
+// the 92 real-data channels are empty per graph).  chl[g*(C+1)] = count n,
+// chl[g*(C+1) + 1 + i] = i-th channel with an edge, ascending.  A channel is
+// empty iff every in-degree is zero (deg holds exact row sums).
+#define CHL_MAXC 4096
+// Block 0 also writes the identity list [C, 0, 1, .., C-1] at chl_all (the
+// dense channel loop, GGNN_DENSE_CHANNELS: read with graph stride 0).
+template <int V>
+__global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, int C, int* __restrict__ chl,
+                                                   int* __restrict__ chl_all) {
+  __shared__ unsigned char fl[CHL_MAXC];
+  const int g = blockIdx.x;
+  if (g == 0) {
+    for (int c = threadIdx.x; c < C; c += 256) chl_all[1 + c] = c;
+    if (threadIdx.x == 0) chl_all[0] = C;
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const uint4* d = (const uint4*)(deg + ((long)g * C + c) * V);
+    uint32_t any = 0;
+#pragma unroll
+    for (int k = 0; k < V / 8; ++k) {
+      const uint4 x = d[k];
+      any |= x.x | x.y | x.z | x.w;
+    }
+    fl[c] = any != 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* out = chl + (long)g * (C + 1);
+    int n = 0;
+    for (int c = 0; c < C; ++c)
+      if (fl[c]) out[1 + n++] = c;
+    out[0] = n;
+  }
+}
+
 // ---- all weight packs of one ggnn_pack_weights call in ONE launch: a job
 // table of k_pack_B problems (and fp32 copies for the biases); block b runs
 // job j with blk_begin[j] <= b < blk_begin[j+1]

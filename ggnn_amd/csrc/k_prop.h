@@ -20,7 +20,8 @@
 // ===========================================================================
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
-k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, const u16* __restrict__ Wp, long wlo,
+k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, const int* __restrict__ chl, int chs,
+           const u16* __restrict__ Wp, long wlo,
            const float* __restrict__ beta, ActT<PREC>* __restrict__ Xo, u16* __restrict__ XT, int C, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
@@ -36,24 +37,32 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + NAB * A_BYTES];
   char* h_hi = smem;
   char* h_lo = smem + (SPLIT ? IMG : 0);
-  auto abuf_of = [&](int c) { return smem + NIMG * IMG + (NAB == 2 ? (c & 1) * A_BYTES : 0); };
+  auto abuf_of = [&](int i) { return smem + NIMG * IMG + (NAB == 2 ? (i & 1) * A_BYTES : 0); };
 
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, ns = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int n = ns * 32 + l32;
   const long rowg = (long)g * V;
 
+  // channels of this graph with an edge (k_chan_list; the identity list with
+  // chs = 0 for the dense loop): an empty A_c adds exactly zero, so skipping
+  // it is bit-identical
+  const int* cl = chl + (long)g * chs;
+  const int nc = cl[0];
+  auto chan = [&](int i) { return cl[1 + i]; };
+
   stage_rows_k<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
-  glds_tile<ACH, V, NT>(abuf_of(0), ag, tid);
+  if (nc > 0) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)chan(0) * V * V, tid);
   __syncthreads();
-  if (NAB == 2 && C > 1) glds_tile<ACH, V, NT>(abuf_of(1), ag + (long)V * V, tid);
+  if (NAB == 2 && nc > 1) glds_tile<ACH, V, NT>(abuf_of(1), ag + (long)chan(1) * V * V, tid);
 
   f32x16 accx[VT];
 #pragma unroll
   for (int it = 0; it < VT; ++it) accx[it] = splat(0.f);
 
-  for (int c = 0; c < C; ++c) {
+  for (int ci = 0; ci < nc; ++ci) {
+    const int c = chan(ci);
     // ---- MT: M_c[j][n] = sum_k h[j][k] W_c[k][n] + beta_c[n]
     const float bb = beta[c * H + n];
     f32x16 accm[VT];
@@ -77,8 +86,8 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
     __syncthreads();  // S1: A_c visible (two tiles: and every wave is past AGG(c-1))
-    if (NAB == 2 && c >= 1 && c + 1 < C) glds_tile<ACH, V, NT>(abuf_of(c + 1), ag + (long)(c + 1) * V * V, tid);
-    const char* abuf = abuf_of(c);
+    if (NAB == 2 && ci >= 1 && ci + 1 < nc) glds_tile<ACH, V, NT>(abuf_of(ci + 1), ag + (long)chan(ci + 1) * V * V, tid);
+    const char* abuf = abuf_of(ci);
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
     for (int rt = 0; rt < VT; ++rt) {
@@ -95,7 +104,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (NAB == 1) {
       __syncthreads();  // S2: A_c reads done
       // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
-      if (c + 1 < C) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)(c + 1) * V * V, tid);
+      if (ci + 1 < nc) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)chan(ci + 1) * V * V, tid);
     }
   }
 
@@ -142,7 +151,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
-           const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
+           const int* __restrict__ chl, int chs, const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
            u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
            const uint32_t* __restrict__ gmax) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -178,8 +187,12 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     }
   }
 
+  // non-empty channels only (k_chan_list); the others get dM = 0 (end of kernel)
+  const int* cl = chl + (long)g * chs;
+  const int nc = cl[0];
+  auto chan = [&](int i) { return cl[1 + i]; };
   const u16* ag = AbT + (long)g * C * V * V;
-  glds_tile<ACH, V, NT>(abuf, ag, tid);
+  if (nc > 0) glds_tile<ACH, V, NT>(abuf, ag + (long)chan(0) * V * V, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
   const int vo = (4 * hh * H + n) * 4;
   f32x16 adh[VT];
@@ -189,7 +202,8 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     for (int r = 0; r < 16; ++r) adh[jt][r] = bld(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
   __syncthreads();
 
-  for (int c = 0; c < C; ++c) {
+  for (int ci = 0; ci < nc; ++ci) {
+    const int c = chan(ci);
     // ---- phase a: dM_c^T tile (rows n of this wave), one 32-column j tile at a time
     v2u32 dq[VT][4];  // f16(dM^T) quad-transposed for the deferred HBM store
 #pragma unroll
@@ -231,7 +245,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
     // A_{c+1} lands in LDS by DMA while phase b runs (drained by S2)
-    if (c + 1 < C) glds_tile<ACH, V, NT>(abuf, ag + (long)(c + 1) * V * V, tid);
+    if (ci + 1 < nc) glds_tile<ACH, V, NT>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
     auto ldb = [&](int ks) {
@@ -291,6 +305,23 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         x = drop_apply(dr, u4_get(dw, r & 3), x);
       }
       bst(rdo, x, vo, (jt * 32 + acc_row0(r)) * H * 4);
+    }
+  }
+  // empty channels: dM_c = A_c^T dX = 0 exactly.  Their dM^T rows (the graph's
+  // V*H contiguous elements of channel c, wg_off layout) and dbeta partials
+  // are written as zeros for the weight-gradient kernels.
+  if (nc < C) {
+    for (int c = 0, p = 0; c < C; ++c) {
+      if (p < nc && cl[1 + p] == c) {
+        ++p;
+        continue;
+      }
+      if (dMT) {
+        u16* z = dMT + (long)c * H * N + rowg * H;
+        for (int q = tid; q < V * H / 8; q += NT) st16(z + q * 8, make_uint4(0, 0, 0, 0));
+      }
+      if (dbp)
+        for (int q = tid; q < H; q += NT) dbp[((long)g * C + c) * H + q] = 0.f;
     }
   }
 }

@@ -72,6 +72,14 @@ enum {
  *                     arithmetic to <= 1e-3 (tests/test_gpu_parity.py) */
 #define GGNN_FP32_PARITY 2
 #define GGNN_FP16 4
+/* Empty-channel skipping.  The staged adjacency carries a
+ * per-graph list of the channels with at least one edge; the message
+ * transform and aggregation (forward and backward) run only over those, since
+ * an empty A[g,c] contributes exactly zero (the real btb adjacency has
+ * C = 2E = 92 channels, about 60 % of them empty per graph).  Results are
+ * bit-identical to the dense loop.  GGNN_DENSE_CHANNELS turns the skipping
+ * off (A/B measurement and the bit-identity test). */
+#define GGNN_DENSE_CHANNELS 8
 
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
@@ -116,8 +124,9 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack,
                       ggnn_stream_t stream);
 
 /* Stage one batch's adjacency [b][C][v][v] fp32 (0/1) into `adj` (sized by
- * ggnn_adjacency_bytes): bf16 (exact for 0/1), its transpose and per-node
- * in-degrees.  T and flags of d are ignored. */
+ * ggnn_adjacency_bytes): 16-bit (exact for 0/1; bf16, or f16 under GGNN_FP16 /
+ * GGNN_FP32_PARITY), its transpose, per-node in-degrees and the per-graph list
+ * of non-empty channels.  T of d is ignored. */
 int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* adjacency,
                        ggnn_stream_t stream);
 

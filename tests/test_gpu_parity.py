@@ -56,11 +56,11 @@ def _f64(w):
     return {k: x.astype(np.float64) for k, x in w.items()}
 
 
-def _run(A, h0, w, T, precision, use_bias=True, dhT=None):
+def _run(A, h0, w, T, precision, use_bias=True, dhT=None, skip=True):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, C, v, _ = A.shape
-    eng = PropagationEngine(h0.shape[-1], C, use_edge_bias=use_bias, precision=precision)
+    eng = PropagationEngine(h0.shape[-1], C, use_edge_bias=use_bias, precision=precision, skip_empty_channels=skip)
     dev = eng.device
     pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()})
     eng.set_adjacency(torch.from_numpy(np.ascontiguousarray(A)).to(dev))
@@ -590,3 +590,52 @@ def test_edge_dropout_long_unroll_packs_in_several_launches():
     ref, caches = O.forward(A64, h0.astype(np.float64), w64, 12, dropout=dr)
     got = _run_dropout(A, h0, w, 12, "fp32", dr, dhT)
     assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+
+
+def _tree_adjacency(b, v, E, seed):
+    """Dependency-tree-shaped graphs (graph_to_adj_mat_bd, chem_tensorflow_dense.py:65-83)
+    with E labels: most of the 2E channels of a graph are empty, as in the real
+    btb data (~30-38 of 92 non-empty).  Graph 0 has no edge at all."""
+    rng = np.random.default_rng(seed)
+    A = np.zeros((b, 2 * E, v, v), np.float32)
+    for g in range(1, b):
+        n = int(rng.integers(v // 2, v + 1))
+        edges = [(int(rng.integers(0, i)), int(rng.integers(1, E + 1)), i) for i in range(1, n)]
+        A[g] = O.graph_to_adj_mat_bd(edges, v, E, dtype=np.float32)
+    return A
+
+
+@pytest.mark.parametrize("b,v,h,E,T,precision", [
+    (4, 50, 256, 46, 3, "fp32"),     # real-data C = 92, v -> 64: k_prop_fwd / k_prop_bwd
+    (3, 120, 256, 46, 2, "fp32"),    # v -> 128, hidden 256: the fused forward
+    (4, 30, 128, 13, 2, "fp32"),     # nivre->std label set (C = 26), v -> 32
+    (3, 120, 256, 46, 2, "bf16"),
+])
+def test_empty_channel_skipping_is_bit_identical(b, v, h, E, T, precision):
+    """the engine runs MT + AGG only over each graph's
+    non-empty channels (k_chan_list); an empty A_c contributes exactly zero, so
+    h_T and dL/dh0 (atomic-free chains) must equal the dense channel loop's bit
+    for bit.  The weight gradients are summed over graphs / row chunks with fp32
+    atomics (k_wgrad256 split-K, k_sum_graphs), whose order varies from run to
+    run, so they are held to 1e-6 of each other; the fp32 mode must match the
+    oracle."""
+    C = 2 * E
+    A = _tree_adjacency(b, v, E, seed=b + v)
+    assert (A.reshape(b, C, -1).max(-1) > 0).sum(1).max() < C  # some channels really are empty
+    rng = np.random.default_rng(v)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, C, seed=E)
+    dhT = (rng.standard_normal((b, v, h)) * 2.0 ** -10).astype(np.float32)
+    skip = _run(A, h0, w, T, precision, dhT=dhT, skip=True)
+    dense = _run(A, h0, w, T, precision, dhT=dhT, skip=False)
+    for k in ("hT", "h0"):
+        assert np.array_equal(skip[k], dense[k]), k
+    for k in GRADS[1:]:
+        assert _nmax(skip[k], dense[k]) <= 1e-6, (k, _nmax(skip[k], dense[k]))
+    if precision == "fp32":
+        A64, w64 = A.astype(np.float64), _f64(w)
+        ref, caches = O.forward(A64, h0.astype(np.float64), w64, T)
+        gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+        assert np.abs(skip["hT"] - ref).max() <= FP32_TOL
+        for k in GRADS:
+            assert _nmax(skip[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
