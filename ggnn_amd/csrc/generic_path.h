@@ -1,0 +1,349 @@
+// generic_path.h -- host side of the general path (included by ggnn_api.hip
+// inside its anonymous namespace, after Cfg / Prof / Zeroer).
+//
+// Taken for every shape outside the specialised kernels' envelope (hidden
+// size not 128 / 256, v > 128; GGNN_GENERIC forces it): the reference's
+// default hidden_size 400 (chem_tensorflow.py:95), its buckets up to 198 nodes
+// (chem_tensorflow_dense.py:584-585), hidden 64 training.  Every product is a
+// k_gemm launch (MFMA, the same precision policy as the fast path), every
+// element-wise step a k_generic.h kernel; activations fp32, rows unpadded.
+//
+// Per timestep t (chem_tensorflow_dense.py:328-333, :391-437, GRUCell):
+//   M[g,c]  = h_t[g] W_c + beta_c         z = (g, c) over non-empty tiles
+//   X[g]    = sum_c A[g,c] M[g,c]          z = g, terms = g's channel list
+//   G       = sigmoid([X, h] Wg + bg)      two terms (X, h) -> (r | u)
+//   rh      = r h ;  cc = tanh([X, rh] Wc + bc) ;  h_{t+1} = u h + (1-u) cc
+// and the backward of SURVEY.md Appendix A in the same decomposition.
+#pragma once
+
+struct GenAdjL {
+  size_t Ag, occ, chl, cgl, total;
+  int vp;
+};
+GenAdjL gen_adj_layout(const Cfg& c) {
+  GenAdjL L;
+  size_t o = 0;
+  L.vp = (c.vin + 7) & ~7;
+  L.Ag = o;  o += al((size_t)c.b * c.C * c.vin * L.vp * 2);
+  L.occ = o; o += al((size_t)c.b * c.C);
+  L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);
+  L.cgl = o; o += al((size_t)c.C * (c.b + 1) * 4);
+  L.total = o;
+  return L;
+}
+
+struct GenWsL {
+  size_t hs, X, G, RH, CC, M, Dl, DXH, DZC, DZG, DRH, GW, gmax, total;
+  size_t nh, ns;  // floats of one [N][H] array; saved-step slots
+  size_t hsl(int t) const { return hs + (size_t)t * nh * 4; }
+  size_t x(int t) const { return X + (size_t)(t % ns) * nh * 4; }
+  size_t g(int t) const { return G + (size_t)(t % ns) * nh * 8; }
+  size_t rh(int t) const { return RH + (size_t)(t % ns) * nh * 4; }
+  size_t cc(int t) const { return CC + (size_t)(t % ns) * nh * 4; }
+};
+GenWsL gen_ws_layout(const Cfg& c, bool tr) {
+  GenWsL L;
+  memset(&L, 0, sizeof(L));
+  const size_t N = (size_t)c.b * c.vin, H = c.H;
+  L.nh = N * H;
+  L.ns = tr ? c.T : 1;
+  size_t o = 0;
+  const size_t a4 = al(N * H * 4);
+  L.nh = a4 / 4;  // slot stride (256-byte aligned)
+  L.hs = o;  o += a4 * (tr ? c.T + 1 : 2);
+  L.X = o;   o += a4 * L.ns;
+  L.G = o;   o += 2 * a4 * L.ns;
+  L.RH = o;  o += a4 * L.ns;
+  L.CC = o;  o += a4 * L.ns;
+  L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
+  if (tr) {
+    L.Dl = o;  o += a4;
+    L.DXH = o; o += 2 * a4;
+    L.DZC = o; o += a4;
+    L.DZG = o; o += 2 * a4;
+    L.DRH = o; o += a4;
+    if (c.ed) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
+    L.gmax = o; o += al(4);
+  }
+  L.total = o;
+  return L;
+}
+
+GemmArgs gg_args() {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.zdiv = 1;
+  a.Z = 1;
+  a.alpha = 1.0f;
+  return a;
+}
+
+// operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
+// BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
+template <int PREC>
+int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
+  if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
+  if (a.Ktot == 0) a.Ktot = a.K;
+  const dim3 grid((unsigned)((a.N + 63) / 64), (unsigned)((a.M + 63) / 64), (unsigned)std::min(a.Z, 65535));
+  Prof p(kind, s);
+#define GGL(A16_, AKC_, BKC_) hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_>), grid, dim3(256), 0, s, a)
+  if (A16 && AKC && !BKC) GGL(true, true, false);
+  else if (A16 && !AKC && !BKC) GGL(true, false, false);
+  else if (!A16 && AKC && !BKC) GGL(false, true, false);
+  else if (!A16 && AKC && BKC) GGL(false, true, true);
+  else if (!A16 && !AKC && !BKC) GGL(false, false, false);
+  else return fail(GGNN_EINVAL, "k_gemm: operand layout combination not compiled");
+#undef GGL
+  return GGNN_OK;
+}
+
+// ---------------------------------------------------------------- adjacency
+int gen_set_adjacency(const Cfg& c, void* adj, const float* A, hipStream_t s) {
+  const GenAdjL L = gen_adj_layout(c);
+  Prof p(K_ADJ, s);
+  if (c.prec == PREC_BF16)
+    hipLaunchKernelGGL(k_gen_adj<false>, dim3((unsigned)(c.b * c.C)), dim3(256), 0, s, A, c.vin, L.vp,
+                       P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+  else
+    hipLaunchKernelGGL(k_gen_adj<true>, dim3((unsigned)(c.b * c.C)), dim3(256), 0, s, A, c.vin, L.vp,
+                       P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+  return GGNN_OK;
+}
+int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const int32_t* goff, int64_t ne, int E,
+                            hipStream_t s) {
+  const GenAdjL L = gen_adj_layout(c);
+  Prof p(K_ADJ, s);
+  HIPCHK(hipMemsetAsync(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s));
+  HIPCHK(hipMemsetAsync(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C, s));
+  if (ne > 0)
+    hipLaunchKernelGGL(k_gen_adj_edges, dim3((unsigned)std::min(c.b, 4096)), dim3(256), 0, s, edges, goff, c.b, c.vin,
+                       L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+  return GGNN_OK;
+}
+// channel lists of the staged batch (per graph, per channel); rebuilt by every
+// forward so that GGNN_DENSE_CHANNELS can be chosen per call
+void gen_lists(const Cfg& c, void* adj, hipStream_t s) {
+  const GenAdjL L = gen_adj_layout(c);
+  const int n = c.b + c.C;
+  hipLaunchKernelGGL(k_gen_lists, dim3((n + 255) / 256), dim3(256), 0, s, P<const unsigned char>(adj, L.occ), c.b,
+                     c.C, (c.flags & GGNN_DENSE_CHANNELS) ? 1 : 0, P<int>(adj, L.chl), P<int>(adj, L.cgl));
+}
+
+// -------------------------------------------------------------------- forward
+template <int PREC>
+int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, const float* h0, float* hT,
+                hipStream_t s) {
+  const GenAdjL AL = gen_adj_layout(c);
+  const PackL PL = pack_layout(c);
+  const GenWsL L = gen_ws_layout(c, tr);
+  const long N = (long)c.b * c.vin, H = c.H, v = c.vin, C = c.C;
+  const bool dense_ch = (c.flags & GGNN_DENSE_CHANNELS) != 0;
+  gen_lists(c, adj, s);
+  {
+    Prof p(K_IO, s);
+    HIPCHK(hipMemcpyAsync(P<float>(ws, L.hsl(0)), h0, (size_t)N * H * 4, hipMemcpyDeviceToDevice, s));
+  }
+  const float* beta = (c.flags & GGNN_USE_EDGE_BIAS) ? P<float>(pack, PL.beta) : nullptr;
+  for (int t = 0; t < c.T; ++t) {
+    const size_t hin = tr ? L.hsl(t) : L.hsl(t & 1);
+    float* hout = (t + 1 == c.T) ? hT : P<float>(ws, tr ? L.hsl(t + 1) : L.hsl((t + 1) & 1));
+    // M[g,c] = h_t[g] W_c + beta_c over the non-empty (g, c) tiles
+    GemmArgs m = gg_args();
+    m.A = P<float>(ws, hin); m.sAp = v * H; m.sAm = H; m.sAk = 1;
+    m.B = P<float>(pack, PL.gw(c.ed ? t : 0)); m.sBq = H * H; m.sBk = H; m.sBn = 1;
+    m.D = P<float>(ws, L.M); m.sDz = v * H; m.sDm = H; m.sDn = 1;
+    m.bias = beta; m.sbq = H;
+    m.zdiv = (int)C; m.Z = (int)(c.b * C); m.zmask = dense_ch ? nullptr : P<unsigned char>(adj, AL.occ);
+    m.M = (int)v; m.N = (int)H; m.K = (int)H;
+    if (int e = gg_launch<PREC>(m, false, true, false, K_PROP_FWD, s)) return e;
+    // X[g] = sum over g's channels of A[g,c] M[g,c]
+    GemmArgs x = gg_args();
+    x.A = P<u16>(adj, AL.Ag); x.sAp = C * v * AL.vp; x.sAq = v * AL.vp; x.sAm = AL.vp; x.sAk = 1;
+    x.B = P<float>(ws, L.M); x.sBp = C * v * H; x.sBq = v * H; x.sBk = H; x.sBn = 1;
+    x.D = P<float>(ws, L.x(t)); x.sDz = v * H; x.sDm = H; x.sDn = 1;
+    x.tl = P<int>(adj, AL.chl); x.ts = C + 1;
+    x.Z = c.b; x.M = (int)v; x.N = (int)H; x.K = (int)v;
+    if (int e = gg_launch<PREC>(x, true, true, false, K_PROP_FWD, s)) return e;
+    // gates = sigmoid([X, h] Wg + bg)
+    GemmArgs gt = gg_args();
+    gt.A = P<float>(ws, L.x(t)); gt.sAq = ((long)hin - (long)L.x(t)) / 4; gt.sAm = H; gt.sAk = 1;
+    gt.B = P<float>(pack, PL.gWg); gt.sBq = H * 2 * H; gt.sBk = 2 * H; gt.sBn = 1;
+    gt.D = P<float>(ws, L.g(t)); gt.sDm = 2 * H; gt.sDn = 1;
+    gt.bias = P<float>(pack, PL.bg);
+    gt.tl = P<int>(pack, PL.two); gt.ts = 0;
+    gt.M = (int)N; gt.N = (int)(2 * H); gt.K = (int)H; gt.epi = GG_EPI_SIGMOID;
+    if (int e = gg_launch<PREC>(gt, false, true, false, K_GRU_FWD, s)) return e;
+    {
+      Prof p(K_GRU_FWD, s);
+      hipLaunchKernelGGL(k_gen_rh, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
+                         P<const float>(ws, hin), P<float>(ws, L.rh(t)), N, c.H);
+    }
+    // cc = tanh([X, r h] Wc + bc)
+    GemmArgs cd = gg_args();
+    cd.A = P<float>(ws, L.x(t)); cd.sAq = ((long)L.rh(t) - (long)L.x(t)) / 4; cd.sAm = H; cd.sAk = 1;
+    cd.B = P<float>(pack, PL.gWc); cd.sBq = H * H; cd.sBk = H; cd.sBn = 1;
+    cd.D = P<float>(ws, L.cc(t)); cd.sDm = H; cd.sDn = 1;
+    cd.bias = P<float>(pack, PL.bc);
+    cd.tl = P<int>(pack, PL.two); cd.ts = 0;
+    cd.M = (int)N; cd.N = (int)H; cd.K = (int)H; cd.epi = GG_EPI_TANH;
+    if (int e = gg_launch<PREC>(cd, false, true, false, K_GRU_FWD, s)) return e;
+    {
+      Prof p(K_GRU_FWD, s);
+      hipLaunchKernelGGL(k_gen_blend, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
+                         P<const float>(ws, hin), P<const float>(ws, L.cc(t)), hout, N, c.H, c.vin, c.sdrop, t);
+    }
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+// ------------------------------------------------------------------- backward
+template <int PREC>
+int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const float* dhT, float* dh0, float* dW,
+                 float* dbeta, float* dWg, float* dbg, float* dWc, float* dbc, hipStream_t s) {
+  const GenAdjL AL = gen_adj_layout(c);
+  const PackL PL = pack_layout(c);
+  const GenWsL L = gen_ws_layout(c, true);
+  const long N = (long)c.b * c.vin, H = c.H, v = c.vin, C = c.C;
+  const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
+  const bool dense_ch = (c.flags & GGNN_DENSE_CHANNELS) != 0;
+  {
+    Prof p(K_IO, s);
+    Zeroer z(s);
+    z.add(dW, C * H * H);
+    z.add(dWg, 4 * H * H);
+    z.add(dbg, 2 * H);
+    z.add(dWc, 2 * H * H);
+    z.add(dbc, H);
+    if (use_bias) z.add(dbeta, C * H);
+    z.add(P<float>(ws, L.gmax), 1);
+  }
+  const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
+  float* Dl = P<float>(ws, L.Dl);
+  float* DXH = P<float>(ws, L.DXH);
+  float* DZC = P<float>(ws, L.DZC);
+  float* DZG = P<float>(ws, L.DZG);
+  float* DRH = P<float>(ws, L.DRH);
+  float* dM = P<float>(ws, L.M);
+  {
+    Prof p(K_IO, s);
+    hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(N * H / 4 + 1), 1024)), dim3(256), 0, s, dhT, N * H,
+                       P<uint32_t>(ws, L.gmax));
+    hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
+                       gmax);
+  }
+  // split-K chunk of the weight-gradient products over the N rows
+  const long KC = std::max<long>(256, ((N + 63) / 64 + 31) & ~31L);
+  const int nkc = (int)((N + KC - 1) / KC);
+  for (int t = c.T - 1; t >= 0; --t) {
+    const float* ht = P<float>(ws, L.hsl(t));
+    const float* G = P<float>(ws, L.g(t));
+    {
+      Prof p(K_GRU_BWD, s);
+      hipLaunchKernelGGL(k_gen_bwd1, dim3(grid1d(N * H)), dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)),
+                         DZC, DZG, DXH, N, c.H);
+    }
+    // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k])
+    for (int half = 0; half < 2; ++half) {
+      GemmArgs a = gg_args();
+      a.A = DZC; a.sAm = H; a.sAk = 1;
+      a.B = P<float>(pack, PL.gWc) + half * H * H; a.sBk = 1; a.sBn = H;
+      a.D = half ? DRH : DXH; a.sDm = half ? H : 2 * H; a.sDn = 1;
+      a.M = (int)N; a.N = (int)H; a.K = (int)H;
+      if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
+    }
+    {
+      Prof p(K_GRU_BWD, s);
+      hipLaunchKernelGGL(k_gen_bwd2, dim3(grid1d(N * H)), dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H);
+    }
+    // [dX | dh] += dzg Wg^T
+    {
+      GemmArgs a = gg_args();
+      a.A = DZG; a.sAm = 2 * H; a.sAk = 1;
+      a.B = P<float>(pack, PL.gWg); a.sBk = 1; a.sBn = 2 * H;
+      a.D = DXH; a.sDm = 2 * H; a.sDn = 1; a.mode = GG_ADD;
+      a.M = (int)N; a.N = (int)(2 * H); a.K = (int)(2 * H);
+      if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
+    }
+    // GRU weight gradients: split-K over row chunks, atomics
+    auto wg = [&](const float* Aop, const float* Bop, long ldB, int Nn, float* out, long ldO) {
+      GemmArgs a = gg_args();
+      a.A = Aop; a.sAp = KC * H; a.sAm = 1; a.sAk = H;
+      a.B = Bop; a.sBp = KC * ldB; a.sBk = ldB; a.sBn = 1;
+      a.D = out; a.sDm = ldO; a.sDn = 1; a.mode = GG_ATOMIC;
+      a.Z = nkc; a.M = (int)H; a.N = Nn; a.K = (int)KC; a.Ktot = N; a.sKp = KC;
+      return gg_launch<PREC>(a, false, false, false, K_WGRAD, s);
+    };
+    if (int e = wg(P<float>(ws, L.x(t)), DZC, H, (int)H, dWc, H)) return e;
+    if (int e = wg(P<float>(ws, L.rh(t)), DZC, H, (int)H, dWc + H * H, H)) return e;
+    if (int e = wg(P<float>(ws, L.x(t)), DZG, 2 * H, (int)(2 * H), dWg, 2 * H)) return e;
+    if (int e = wg(ht, DZG, 2 * H, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
+    {
+      Prof p(K_WGRAD, s);
+      const unsigned ys = (unsigned)std::max<long>(1, std::min<long>(256, N / 64));
+      hipLaunchKernelGGL(k_gen_colsum, dim3((unsigned)((H + 255) / 256), ys), dim3(256), 0, s, DZC, N, c.H, H, dbc);
+      hipLaunchKernelGGL(k_gen_colsum, dim3((unsigned)((2 * H + 255) / 256), ys), dim3(256), 0, s, DZG, N,
+                         (int)(2 * H), 2 * H, dbg);
+    }
+    // dM[g,c] = A[g,c]^T dX[g] over the non-empty tiles
+    {
+      GemmArgs a = gg_args();
+      a.A = P<u16>(adj, AL.Ag); a.sAp = C * v * AL.vp; a.sAq = v * AL.vp; a.sAm = 1; a.sAk = AL.vp;
+      a.B = DXH; a.sBp = v * 2 * H; a.sBk = 2 * H; a.sBn = 1;
+      a.D = dM; a.sDz = v * H; a.sDm = H; a.sDn = 1;
+      a.zdiv = (int)C; a.Z = (int)(c.b * C); a.zmask = dense_ch ? nullptr : P<unsigned char>(adj, AL.occ);
+      a.M = (int)v; a.N = (int)H; a.K = (int)v;
+      if (int e = gg_launch<PREC>(a, true, false, false, K_PROP_BWD, s)) return e;
+    }
+    // dh[g] += sum over g's channels of dM[g,c] W_c^T
+    {
+      GemmArgs a = gg_args();
+      a.A = dM; a.sAp = C * v * H; a.sAq = v * H; a.sAm = H; a.sAk = 1;
+      a.B = P<float>(pack, PL.gw(c.ed ? t : 0)); a.sBq = H * H; a.sBk = 1; a.sBn = H;
+      a.D = DXH + H; a.sDz = v * 2 * H; a.sDm = 2 * H; a.sDn = 1; a.mode = GG_ADD;
+      a.tl = P<int>(adj, AL.chl); a.ts = C + 1;
+      a.Z = c.b; a.M = (int)v; a.N = (int)H; a.K = (int)H;
+      if (int e = gg_launch<PREC>(a, false, true, true, K_PROP_BWD, s)) return e;
+    }
+    // dW_c (+)= sum over c's graphs of h_t[g]^T dM[g,c]; dbeta_c += column sums of dM[g,c]
+    {
+      float* G_out = c.ed ? P<float>(ws, L.GW) : dW;
+      GemmArgs a = gg_args();
+      a.A = ht; a.sAq = v * H; a.sAm = 1; a.sAk = H;
+      a.B = dM; a.sBp = v * H; a.sBq = C * v * H; a.sBk = H; a.sBn = 1;
+      a.D = G_out; a.sDz = H * H; a.sDm = H; a.sDn = 1; a.mode = c.ed ? GG_STORE : GG_ADD;
+      a.tl = P<int>(adj, AL.cgl); a.ts = c.b + 1;
+      a.Z = (int)C; a.M = (int)H; a.N = (int)H; a.K = (int)v;
+      if (int e = gg_launch<PREC>(a, false, false, false, K_WGRAD, s)) return e;
+      Prof p(K_WGRAD, s);
+      if (c.ed)
+        hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * H * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
+                           c.C, c.H, t, c.edrop);
+      if (use_bias)
+        hipLaunchKernelGGL(k_gen_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C), dim3(256), 0, s, dM,
+                           P<const int>(adj, AL.cgl), c.b, c.C, c.vin, c.H, dbeta);
+    }
+    // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
+    {
+      Prof p(K_PROP_BWD, s);
+      hipLaunchKernelGGL(k_gen_delta, dim3(grid1d(N * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
+                         c.sdrop, t - 1, gmax, t == 0 ? 1 : 0);
+    }
+  }
+  {
+    Prof p(K_IO, s);
+    ZeroJobs j;
+    memset(&j, 0, sizeof(j));
+    int nj = 0;
+    auto add = [&](float* p_, long n) { j.p[nj] = p_; j.n[nj++] = n; };
+    add(dW, C * H * H);
+    add(dWg, 4 * H * H);
+    add(dbg, 2 * H);
+    add(dWc, 2 * H * H);
+    add(dbc, H);
+    if (use_bias) add(dbeta, C * H);
+    hipLaunchKernelGGL(k_unscale_multi, dim3(128, nj), dim3(256), 0, s, j, gmax);
+  }
+  LAUNCHCHK();
+  return GGNN_OK;
+}

@@ -20,6 +20,8 @@
 #include "k_optim.h"
 #include "k_wgrad.h"
 #include "k_head.h"
+#include "k_gemm.h"
+#include "k_generic.h"
 
 // ---------------------------------------------------------------------------
 // error handling (thread-local last error; no exception crosses the ABI)
@@ -79,6 +81,7 @@ struct Cfg {
   int vsh;  // log2(V)
   Drop edrop, sdrop;  // edge-weight / state dropout (thr == 0: off)
   bool ed, sd;
+  bool generic;       // the general path (generic_path.h)
 };
 
 Drop make_drop(float keep, uint64_t seed) {
@@ -101,12 +104,13 @@ int pad_v(int v) { return v <= 32 ? 32 : v <= 64 ? 64 : v <= 128 ? 128 : -1; }
 int make_cfg(const ggnn_dims* d, Cfg* c) {
   if (!d) return fail(GGNN_EINVAL, "dims is NULL");
   if (d->b < 1 || d->v < 1 || d->C < 1 || d->T < 1) return fail(GGNN_EINVAL, "dims: b, v, C, T must be >= 1");
-  if (!(d->h == 64 || d->h == 128 || d->h == 256))
-    return fail(GGNN_EUNSUP, "hidden size must be 64, 128 or 256 (got " + std::to_string(d->h) + ")");
-  const int V = pad_v(d->v);
-  if (V < 0) return fail(GGNN_EUNSUP, "v must be <= 128 (got " + std::to_string(d->v) + ")");
-  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS))
+  if (d->h < 1 || d->h > 4096) return fail(GGNN_EUNSUP, "hidden size must lie in 1..4096 (got " + std::to_string(d->h) + ")");
+  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS | GGNN_GENERIC))
     return fail(GGNN_EINVAL, "unknown flag bits");
+  // the specialised kernels: hidden 128 / 256, v <= 128; everything else runs
+  // the general path (generic_path.h)
+  c->generic = (d->flags & GGNN_GENERIC) || !(d->h == 128 || d->h == 256) || d->v > 128;
+  const int V = c->generic ? d->v : pad_v(d->v);
   if (d->C > CHL_MAXC) return fail(GGNN_EUNSUP, "C must be <= " + std::to_string(CHL_MAXC));
   if ((d->flags & GGNN_FP32_PARITY) && (d->flags & GGNN_FP16))
     return fail(GGNN_EINVAL, "GGNN_FP32_PARITY and GGNN_FP16 are exclusive");
@@ -115,7 +119,7 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   c->split = c->prec == PREC_SPLIT;
   c->act = c->split ? 4 : 2;
   c->N = (long)d->b * V;
-  c->vsh = V == 32 ? 5 : V == 64 ? 6 : 7;
+  c->vsh = V == 32 ? 5 : V == 64 ? 6 : V == 128 ? 7 : 0;
   if (!(d->edge_keep > 0.0f && d->edge_keep <= 1.0f) || !(d->state_keep > 0.0f && d->state_keep <= 1.0f))
     return fail(GGNN_EINVAL, "dropout keep probabilities must lie in (0, 1] (edge_keep " +
                                  std::to_string(d->edge_keep) + ", state_keep " + std::to_string(d->state_keep) + ")");
@@ -123,7 +127,8 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   c->sdrop = make_drop(d->state_keep, d->seed);
   c->ed = c->edrop.thr != 0;
   c->sd = c->sdrop.thr != 0;
-  if ((double)c->N * c->H * 4 >= 2147483647.0) return fail(GGNN_EUNSUP, "b*v*h too large for 32-bit buffer offsets");
+  if (!c->generic && (double)c->N * c->H * 4 >= 2147483647.0)
+    return fail(GGNN_EUNSUP, "b*v*h too large for 32-bit buffer offsets");
   return GGNN_OK;
 }
 
@@ -132,30 +137,45 @@ size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // ---- weight pack: bf16 hi part then lo part of every packed operand
 // Under edge-weight dropout Wf / WT hold one masked copy per timestep
 // (szW bytes apart).
+// A pack serves every batch shape of one hidden size (bucketed batches have
+// different v), so it holds the specialised kernels' fragment layouts when the
+// hidden size has them (fast) AND the general path's fp32 copies.
 struct PackL {
-  size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, total, szW;
+  bool fast;
+  size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, szW;
+  size_t gW, gszW, gWg, gWc, two, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc
   long loW, loWg, loWc;  // element offset of the lo part from the hi part
   size_t wf(int t) const { return Wf + (size_t)t * szW; }
   size_t wt(int t) const { return WT + (size_t)t * szW; }
+  size_t gw(int t) const { return gW + (size_t)t * gszW; }
 };
 PackL pack_layout(const Cfg& c) {
   PackL L;
+  memset(&L, 0, sizeof(L));
   size_t o = 0;
   const size_t H = c.H;
+  L.fast = (c.H == 128 || c.H == 256) && !(c.flags & GGNN_GENERIC);
   L.loW = (long)c.C * H * H;
   L.loWg = (long)4 * H * H;
   L.loWc = (long)2 * H * H;
   const int nW = c.ed ? c.T : 1;
-  L.szW = al(2 * c.C * H * H * 2);
-  L.Wf = o;   o += L.szW * nW;
-  L.WT = o;   o += L.szW * nW;
+  if (L.fast) {
+    L.szW = al(2 * c.C * H * H * 2);
+    L.Wf = o;   o += L.szW * nW;
+    L.WT = o;   o += L.szW * nW;
+    L.Wg = o;   o += al(2 * 4 * H * H * 2);
+    L.WgT = o;  o += al(2 * 4 * H * H * 2);
+    L.Wc = o;   o += al(2 * 2 * H * H * 2);
+    L.WcT = o;  o += al(2 * 2 * H * H * 2);
+  }
   L.beta = o; o += al(c.C * H * 4);
-  L.Wg = o;   o += al(2 * 4 * H * H * 2);
-  L.WgT = o;  o += al(2 * 4 * H * H * 2);
-  L.Wc = o;   o += al(2 * 2 * H * H * 2);
-  L.WcT = o;  o += al(2 * 2 * H * H * 2);
   L.bg = o;   o += al(2 * H * 4);
   L.bc = o;   o += al(H * 4);
+  L.gszW = al((size_t)c.C * H * H * 4);
+  L.gW = o;   o += L.gszW * nW;
+  L.gWg = o;  o += al(4 * H * H * 4);
+  L.gWc = o;  o += al(2 * H * H * 4);
+  L.two = o;  o += al(3 * 4);  // the term list [2, 0, 1] of the general path's two-operand GRU products
   L.total = o;
   return L;
 }
@@ -630,6 +650,8 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   return GGNN_OK;
 }
 
+#include "generic_path.h"
+
 }  // namespace
 
 // ===========================================================================
@@ -689,7 +711,7 @@ int ggnn_workspace_bytes(const ggnn_dims* d, int training, size_t* bytes) {
   int e = make_cfg(d, &c);
   if (e) return e;
   if (!bytes) return fail(GGNN_EINVAL, "bytes is NULL");
-  *bytes = ws_layout(c, training != 0).total;
+  *bytes = c.generic ? gen_ws_layout(c, training != 0).total : ws_layout(c, training != 0).total;
   return GGNN_OK;
 }
 
@@ -698,7 +720,7 @@ int ggnn_adjacency_bytes(const ggnn_dims* d, size_t* bytes) {
   int e = make_cfg(d, &c);
   if (e) return e;
   if (!bytes) return fail(GGNN_EINVAL, "bytes is NULL");
-  *bytes = adj_layout(c).total;
+  *bytes = c.generic ? gen_adj_layout(c).total : adj_layout(c).total;
   return GGNN_OK;
 }
 
@@ -745,24 +767,31 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
     a.blk_begin[a.count++] = nb;
     nb += (int)((J.total + 255) / 256);
   };
-  auto copy = [&](const float* S, float* out, long n) {
+  auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
     if (a.count == PACK_MAXJ) flush();
     PackJob& J = a.j[a.count];
-    J.S = S; J.out = (u16*)out; J.total = n; J.copy = 1;
+    J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop;
     a.blk_begin[a.count++] = nb;
     nb += (int)((n + 255) / 256);
   };
-  for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
-    job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
-    job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
+  if (L.fast) {
+    for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
+      job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
+      job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
+    }
+    job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
+    job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
+    job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
+    job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
   }
-  job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
-  job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
-  job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
-  job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
   copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
   copy(bg, P<float>(pack, L.bg), 2L * H);
   copy(bc, P<float>(pack, L.bc), (long)H);
+  // the general path's fp32 operands (generic_path.h)
+  for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
+  copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
+  copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
+  copy(nullptr, P<float>(pack, L.two), 3, 3);
   flush();
   LAUNCHCHK();
   return GGNN_OK;
@@ -833,6 +862,11 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
     return fail(GGNN_EINVAL, "set_adjacency_edges: C must equal 2 * num_edge_types");
   if (num_edges < 0) return fail(GGNN_EINVAL, "set_adjacency_edges: num_edges < 0");
   hipStream_t s = (hipStream_t)stream;
+  if (c.generic) {
+    if (int e2 = gen_set_adjacency_edges(c, adj, edges, graph_offsets, num_edges, num_edge_types, s)) return e2;
+    LAUNCHCHK();
+    return GGNN_OK;
+  }
   const AdjL L = adj_layout(c);
   const size_t tiles = (size_t)c.b * c.C;
   Prof p(K_ADJ, s);
@@ -864,6 +898,11 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
   if (e) return e;
   if (!adj || !A) return fail(GGNN_EINVAL, "set_adjacency: NULL pointer");
   hipStream_t s = (hipStream_t)stream;
+  if (c.generic) {
+    if (int e2 = gen_set_adjacency(c, adj, A, s)) return e2;
+    LAUNCHCHK();
+    return GGNN_OK;
+  }
   const AdjL L = adj_layout(c);
   const dim3 grid((unsigned)(c.b * c.C));
   Prof p(K_ADJ, s);
@@ -895,6 +934,14 @@ int ggnn_forward(const ggnn_dims* d, const void* pack, const void* adj, void* ws
   if (e) return e;
   if (!pack || !adj || !ws || !h0 || !hT) return fail(GGNN_EINVAL, "forward: NULL pointer");
   hipStream_t s = (hipStream_t)stream;
+  if (c.generic) {
+    void* adjw = const_cast<void*>(adj);  // (the channel lists are rebuilt per call)
+    switch (c.prec) {
+      case PREC_SPLIT: return gen_forward<PREC_SPLIT>(c, pack, adjw, ws, training != 0, h0, hT, s);
+      case PREC_F16: return gen_forward<PREC_F16>(c, pack, adjw, ws, training != 0, h0, hT, s);
+      default: return gen_forward<PREC_BF16>(c, pack, adjw, ws, training != 0, h0, hT, s);
+    }
+  }
   switch (c.prec) {
     case PREC_SPLIT: return forward_impl<PREC_SPLIT>(c, pack, adj, ws, training != 0, h0, hT, s);
     case PREC_F16: return forward_impl<PREC_F16>(c, pack, adj, ws, training != 0, h0, hT, s);
@@ -912,6 +959,14 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
   if ((c.flags & GGNN_USE_EDGE_BIAS) && !dbeta)
     return fail(GGNN_EINVAL, "backward: d_edge_biases NULL with USE_EDGE_BIAS");
   hipStream_t s = (hipStream_t)stream;
+  if (c.generic) {
+    void* adjw = const_cast<void*>(adj);
+    switch (c.prec) {
+      case PREC_SPLIT: return gen_backward<PREC_SPLIT>(c, pack, adjw, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+      case PREC_F16: return gen_backward<PREC_F16>(c, pack, adjw, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+      default: return gen_backward<PREC_BF16>(c, pack, adjw, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
+    }
+  }
   switch (c.prec) {
     case PREC_SPLIT: return backward_impl<PREC_SPLIT>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);
     case PREC_F16: return backward_impl<PREC_F16>(c, pack, adj, ws, dhT, dh0, dW, dbeta, dWg, dbg, dWc, dbc, s);

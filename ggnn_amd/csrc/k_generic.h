@@ -1,0 +1,212 @@
+// k_generic.h -- the element-wise and staging kernels of the general path
+// (any hidden size, any vertex count; k_gemm.h does the products).  fp32
+// activations, rows = b*v unpadded (row g*v + i = node i of graph g).
+//
+// Reference (chem_tensorflow_dense.py): the T-loop :312-340, the fast step
+// :391-437, the TF1 GRUCell (reset before the matmul, [x, h] concat, r then u)
+// + DropoutWrapper state dropout :237-241, :333; adjacency :65-83.
+#pragma once
+#include "ggnn_common.h"
+
+// ---- adjacency staging: A [b][C][v][v] fp32 (0/1) -> Ag [b][C][v][vp] 16-bit
+// limbs (natural order, row pitch vp = v rounded up to 8) and the per-tile
+// occupancy occ[b*C] (1 = the tile holds an edge).  One block per tile.
+template <bool F16>
+__global__ void __launch_bounds__(256) k_gen_adj(const float* __restrict__ A, int v, int vp, u16* __restrict__ Ag,
+                                                 unsigned char* __restrict__ occ) {
+  const long tile = blockIdx.x;
+  const float* src = A + tile * (long)v * v;
+  u16* dst = Ag + tile * (long)v * vp;
+  int any = 0;
+  for (long q = threadIdx.x; q < (long)v * vp; q += 256) {
+    const int i = (int)(q / vp), j = (int)(q % vp);
+    const float x = j < v ? src[(long)i * v + j] : 0.f;
+    any |= x != 0.f;
+    dst[q] = to_limb<F16>(x);
+  }
+  any = __syncthreads_or(any);
+  if (threadIdx.x == 0) occ[tile] = (unsigned char)(any != 0);
+}
+
+// the same from the reference's edge lists (graph_to_adj_mat_bd semantics,
+// k_prep.h k_adj_from_edges): after a memset of Ag and occ
+__global__ void __launch_bounds__(256) k_gen_adj_edges(const int* __restrict__ edges, const int* __restrict__ goff,
+                                                       int b, int v, int vp, int E, int f16, u16* __restrict__ Ag,
+                                                       unsigned char* __restrict__ occ) {
+  const int C = 2 * E;
+  const u16 one = f16 ? (u16)0x3C00 : (u16)0x3F80;
+  for (int g = blockIdx.x; g < b; g += gridDim.x) {
+    for (int e = goff[g] + threadIdx.x; e < goff[g + 1]; e += 256) {
+      const int src = edges[3 * e], lab = edges[3 * e + 1], dst = edges[3 * e + 2];
+      if (lab < 1 || lab > E || src < 0 || src >= v || dst < 0 || dst >= v) continue;
+      const int prv = dst - 1 < 0 ? v - 1 : dst - 1;  // numpy's wrap of index -1
+      const int ch[4] = {lab - 1, lab - 1 + E, E - 1, 2 * E - 1};
+      const int ro[4] = {dst, src, dst, prv};
+      const int co[4] = {src, dst, prv, dst};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long tile = (long)g * C + ch[k];
+        Ag[(tile * v + ro[k]) * vp + co[k]] = one;
+        occ[tile] = 1;
+      }
+    }
+  }
+}
+
+// per-graph channel lists chl[g*(C+1)] = (count, channels...) and per-channel
+// graph lists cgl[c*(b+1)] = (count, graphs...) from occ; with dense != 0
+// every tile counts as occupied (GGNN_DENSE_CHANNELS)
+__global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C, int dense, int* __restrict__ chl,
+                            int* __restrict__ cgl) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < b) {
+    int* o = chl + (long)t * (C + 1);
+    int n = 0;
+    for (int c = 0; c < C; ++c)
+      if (dense || occ[(long)t * C + c]) o[1 + n++] = c;
+    o[0] = n;
+  } else if (t < b + C) {
+    const int c = t - b;
+    int* o = cgl + (long)c * (b + 1);
+    int n = 0;
+    for (int g = 0; g < b; ++g)
+      if (dense || occ[(long)g * C + c]) o[1 + n++] = g;
+    o[0] = n;
+  }
+}
+
+// ---- weights: fp32 copies, W masked per timestep under edge-weight dropout
+// (the fast path's Philox counter: (i>>2, j, c, t), word i&3)
+__global__ void k_gen_wmask(const float* __restrict__ W, float* __restrict__ out, int C, int H, int t, Drop dr) {
+  const long total = (long)C * H * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % H), i = (int)((e / H) % H), c = (int)(e / ((long)H * H));
+    float x = W[e];
+    if (dr.thr) x = drop_apply(dr, u4_get(edge_words(dr, c, i, j, t), i & 3), x);
+    out[e] = x;
+  }
+}
+// dW[c][i][j] += mask_t / keep * G[c][i][j]   (edge dropout backward, one timestep)
+__global__ void k_gen_wmask_acc(const float* __restrict__ G, float* __restrict__ dW, int C, int H, int t, Drop dr) {
+  const long total = (long)C * H * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % H), i = (int)((e / H) % H), c = (int)(e / ((long)H * H));
+    dW[e] += drop_apply(dr, u4_get(edge_words(dr, c, i, j, t), i & 3), G[e]);
+  }
+}
+
+// ---- forward element-wise steps (G = sigmoid gates [N][2H] = (r | u))
+// rh = r * h
+__global__ void k_gen_rh(const float* __restrict__ G, const float* __restrict__ h, float* __restrict__ rh, long N,
+                         int H) {
+  const long total = N * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    rh[e] = G[row * 2 * H + k] * h[e];
+  }
+}
+// h' = u h + (1 - u) c, then the DropoutWrapper state dropout of timestep t
+__global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict__ h, const float* __restrict__ cc,
+                            float* __restrict__ hout, long N, int H, int v, Drop sd, int t) {
+  const long total = N * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    const float u = G[row * 2 * H + H + k];
+    float x = u * h[e] + (1.0f - u) * cc[e];
+    if (sd.thr) {
+      const int g = (int)(row / v), i = (int)(row % v);
+      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, t), i & 3), x);
+    }
+    hout[e] = x;
+  }
+}
+
+// ---- backward element-wise steps, timestep t (Appendix A of SURVEY.md):
+// e1: dc = d(1-u); du = d(h-c); dzc = dc(1-c^2); dzg_u = du u(1-u);
+//     dh (second half of the [N][2H] buffer DXH) = d u
+__global__ void k_gen_bwd1(const float* __restrict__ d, const float* __restrict__ G, const float* __restrict__ h,
+                           const float* __restrict__ cc, float* __restrict__ dzc, float* __restrict__ dzg,
+                           float* __restrict__ DXH, long N, int H) {
+  const long total = N * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    const float u = G[row * 2 * H + H + k], c = cc[e], dl = d[e];
+    dzc[e] = dl * (1.0f - u) * (1.0f - c * c);
+    dzg[row * 2 * H + H + k] = dl * (h[e] - c) * u * (1.0f - u);
+    DXH[row * 2 * H + H + k] = dl * u;
+  }
+}
+// e2: d(rh) -> dr = d(rh) h, dzg_r = dr r(1-r); dh += d(rh) r
+__global__ void k_gen_bwd2(const float* __restrict__ drh, const float* __restrict__ G, const float* __restrict__ h,
+                           float* __restrict__ dzg, float* __restrict__ DXH, long N, int H) {
+  const long total = N * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    const float r = G[row * 2 * H + k], x = drh[e];
+    dzg[row * 2 * H + k] = x * h[e] * r * (1.0f - r);
+    DXH[row * 2 * H + H + k] += x * r;
+  }
+}
+// dL/dh_t (second half of DXH) -> the next (earlier) step's delta: the state
+// dropout backward of timestep tm = t-1 (tm < 0: none), times osc (the
+// gradient unscale on the last step, else 1)
+__global__ void k_gen_delta(const float* __restrict__ DXH, float* __restrict__ out, long N, int H, int v, Drop sd,
+                            int tm, const uint32_t* __restrict__ gmax, int unscale) {
+  const long total = N * H;
+  const float osc = unscale ? gunscale(gmax) : 1.0f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    float x = DXH[row * 2 * H + H + k] * osc;
+    if (sd.thr && tm >= 0) {
+      const int g = (int)(row / v), i = (int)(row % v);
+      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, tm), i & 3), x);
+    }
+    out[e] = x;
+  }
+}
+// dL/dh_T staging: delta = S * dL/dh_T (gradient scale), state dropout of T-1
+__global__ void k_gen_delta0(const float* __restrict__ dhT, float* __restrict__ out, long N, int H, int v, Drop sd,
+                             int tm, const uint32_t* __restrict__ gmax) {
+  const long total = N * H;
+  const float sc = gscale(gmax);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    float x = dhT[e] * sc;
+    if (sd.thr) {
+      const long row = e / H;
+      const int k = (int)(e % H);
+      const int g = (int)(row / v), i = (int)(row % v);
+      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, tm), i & 3), x);
+    }
+    out[e] = x;
+  }
+}
+
+// column sums: out[n] += sum_rows X[row][n] (ld columns), rows split over
+// blockIdx.y with atomics
+__global__ void k_gen_colsum(const float* __restrict__ X, long rows, int ncol, long ld, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= ncol) return;
+  const long per = (rows + gridDim.y - 1) / gridDim.y;
+  const long r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += X[r * ld + n];
+  if (r1 > r0) atomicAdd(out + n, s);
+}
+// dbeta[c][n] += sum over the graphs g of channel c and nodes j of dM[g][c][j][n]
+__global__ void k_gen_dbeta(const float* __restrict__ dM, const int* __restrict__ cgl, int b, int C, int v, int H,
+                            float* __restrict__ dbeta) {
+  const int c = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= H) return;
+  const int* L = cgl + (long)c * (b + 1);
+  float s = 0.f;
+  for (int e = 0; e < L[0]; ++e) {
+    const float* p = dM + ((long)L[1 + e] * C + c) * v * H + n;
+    for (int j = 0; j < v; ++j) s += p[(long)j * H];
+  }
+  dbeta[(long)c * H + n] += s;
+}

@@ -349,8 +349,21 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
   const PackJob& J = a.j[ji];
   const long q = (long)(blockIdx.x - a.blk_begin[ji]) * 256 + threadIdx.x;
   if (q >= J.total) return;
-  if (J.copy) {
+  if (J.copy == 1) {  // fp32 copy (zeros when S is null)
     ((float*)J.out)[q] = J.S ? J.S[q] : 0.0f;
+    return;
+  }
+  if (J.copy == 2) {  // fp32 copy of W [C][H][H] (H = J.K), edge-dropout mask of timestep J.t when J.drop
+    float x = J.S[q];
+    if (J.drop) {
+      const int H = J.K, wi = (int)((q / H) % H), wj = (int)(q % H), c = (int)(q / ((long)H * H));
+      x = drop_apply(a.dr, u4_get(edge_words(a.dr, c, wi, wj, J.t), wi & 3), x);
+    }
+    ((float*)J.out)[q] = x;
+    return;
+  }
+  if (J.copy == 3) {  // the general path's two-term list [2, 0, 1]
+    ((int*)J.out)[q] = q == 0 ? 2 : (int)q - 1;
     return;
   }
   const int per = (J.N / 32) * (J.K / 16) * 64;  // fragment-lanes per matrix

@@ -80,6 +80,12 @@ enum {
  * bit-identical to the dense loop.  GGNN_DENSE_CHANNELS turns the skipping
  * off (A/B measurement and the bit-identity test). */
 #define GGNN_DENSE_CHANNELS 8
+/* The general path (k_gemm.h + k_generic.h): any hidden size and vertex count.
+ * Taken automatically when hidden is not 128 / 256 or v > 128 (e.g. the
+ * reference's default hidden_size 400, chem_tensorflow.py:95, and its
+ * 198-node buckets, chem_tensorflow_dense.py:584-585); GGNN_GENERIC forces it
+ * for every shape (parity tests, A/B). */
+#define GGNN_GENERIC 16
 
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
@@ -105,8 +111,9 @@ typedef struct ggnn_dims {
 int ggnn_version(void);
 const char* ggnn_last_error(void);
 
-/* Validate dims against the compiled kernel set: 1<=v<=128, h in {64,128,256},
- * C>=1, T>=1, b>=1.  Returns 0 or GGNN_EUNSUP / GGNN_EINVAL. */
+/* Validate dims: b, v, C, T >= 1, 1 <= h <= 4096, C <= 4096.  hidden 128 / 256
+ * with v <= 128 run the specialised kernels, every other shape the general
+ * path.  Returns 0 or GGNN_EUNSUP / GGNN_EINVAL. */
 int ggnn_check_dims(const ggnn_dims* d);
 
 /* Bytes of the per-batch workspace (activations saved for backward when

@@ -1,0 +1,143 @@
+"""GPU parity of the general path (k_gemm products + k_generic.h element-wise
+kernels): the shapes the specialised kernels do not take -- the reference's
+default hidden_size 400 (chem_tensorflow.py:95), buckets beyond 128 nodes up to
+198 (chem_tensorflow_dense.py:584-585), odd hidden sizes, hidden 64 training
+-- against the float64 oracle at the fp32 bar (forward max |err| <= 1e-3,
+every gradient's normalised max error <= 1e-3), with dropout, at the btb
+loss's gradient scale, with empty-channel skipping and from edge lists.
+"""
+import numpy as np
+import pytest
+
+import ggnn_oracle as O
+from test_gpu_parity import (FP32_TOL, GRADS, _case, _f64, _nmax, _nrms, _run, _run_dropout, _torch,
+                             _tree_adjacency)
+
+pytestmark = pytest.mark.gpu
+
+GEN_SHAPES = [
+    (3, 20, 400, 4, 2),     # the reference's default hidden_size
+    (2, 150, 128, 4, 2),    # v > 128
+    (2, 198, 64, 6, 2),     # the reference's largest bucket, hidden 64 (training)
+    (3, 37, 100, 5, 3),     # odd hidden, odd v, odd C
+    (4, 50, 256, 6, 2),     # a fast-path shape, forced through the general path
+]
+
+
+def _ref(A, h0, w, T, dhT):
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T)
+    return ref, O.backward(A64, dhT.astype(np.float64), caches, w64)
+
+
+@pytest.mark.parametrize("b,v,h,C,T", GEN_SHAPES)
+def test_generic_fp32_parity(b, v, h, C, T):
+    A, h0, w = _case(b, v, h, C, seed=b * 11 + v)
+    dhT = np.random.default_rng(2).standard_normal((b, v, h)).astype(np.float32)
+    ref, gref = _ref(A, h0, w, T, dhT)
+    got = _run(A, h0, w, T, "fp32", dhT=dhT, generic=True)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+    inf = _run(A, h0, w, T, "fp32", generic=True)   # inference workspace (no saves)
+    assert np.abs(inf["hT"] - ref).max() <= FP32_TOL
+
+
+@pytest.mark.parametrize("scale", [2.0 ** -12, 2.0 ** -16])
+def test_generic_backward_at_loss_scale(scale):
+    b, v, h, C, T = 2, 150, 400, 4, 3
+    A, h0, w = _case(b, v, h, C, seed=31)
+    dhT = (np.random.default_rng(4).standard_normal((b, v, h)) * scale).astype(np.float32)
+    ref, gref = _ref(A, h0, w, T, dhT)
+    got = _run(A, h0, w, T, "fp32", dhT=dhT)
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
+def test_generic_matches_fast_path():
+    """The config-3 slice through both paths: same math, different kernels."""
+    b, v, h, C, T = 2, 128, 256, 8, 3
+    A, h0, w = _case(b, v, h, C, seed=77)
+    dhT = np.random.default_rng(5).standard_normal((b, v, h)).astype(np.float32)
+    fast = _run(A, h0, w, T, "fp32", dhT=dhT)
+    gen = _run(A, h0, w, T, "fp32", dhT=dhT, generic=True)
+    assert np.abs(fast["hT"] - gen["hT"]).max() <= 5e-5
+    for k in GRADS:
+        # (the fast path's weight-gradient GEMMs take single f16 operands: <= 3.7e-4 vs float64)
+        assert _nmax(gen[k], fast[k]) <= FP32_TOL, k
+
+
+@pytest.mark.parametrize("ek,sk", [(0.9, 0.9), (0.6, 1.0), (1.0, 0.7)])
+def test_generic_dropout_fp32_parity(ek, sk):
+    b, v, h, C, T = 3, 140, 96, 4, 3
+    A, h0, w = _case(b, v, h, C, seed=9)
+    dhT = np.random.default_rng(8).standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=ek, state_keep=sk, seed=1234567 + T)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run_dropout(A, h0, w, T, "fp32", dr, dhT)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+    nodrop, _ = O.forward(A64, h0.astype(np.float64), w64, T, keep_cache=False)
+    assert np.abs(nodrop - ref).max() > 0.05
+
+
+@pytest.mark.parametrize("v,h", [(120, 400), (190, 128)])
+def test_generic_empty_channel_skipping(v, h):
+    """Real-data channel count (C = 92) on the general path: h_T and dL/dh0
+    bit-identical with and without skipping, and fp32 parity."""
+    b, E, T = 3, 46, 2
+    C = 2 * E
+    A = _tree_adjacency(b, v, E, seed=v)
+    rng = np.random.default_rng(h)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, C, seed=E)
+    dhT = (rng.standard_normal((b, v, h)) * 2.0 ** -10).astype(np.float32)
+    skip = _run(A, h0, w, T, "fp32", dhT=dhT, skip=True)
+    dense = _run(A, h0, w, T, "fp32", dhT=dhT, skip=False)
+    for k in ("hT", "h0"):
+        assert np.array_equal(skip[k], dense[k]), k
+    ref, gref = _ref(A, h0, w, T, dhT)
+    assert np.abs(skip["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(skip[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
+def test_generic_adjacency_from_edges():
+    """Edge-list staging on the general path (v = 160 > 128) gives the same
+    forward as the dense feed of graph_to_adj_mat_bd (chem_tensorflow_dense.py:65-83)."""
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    b, v, h, E, T = 3, 160, 128, 5, 2
+    rng = np.random.default_rng(3)
+    graphs = []
+    for _ in range(b):
+        n = int(rng.integers(v // 2, v + 1))
+        graphs.append([(int(rng.integers(0, i)), int(rng.integers(1, E + 1)), i) for i in range(1, n)])
+    graphs[1] = graphs[1] + [(3, 2, 0)]   # dest 0: the reference's prev-word index wraps to v-1
+    A = np.stack([O.graph_to_adj_mat_bd(g, v, E, dtype=np.float32) for g in graphs])
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=1)
+    eng = PropagationEngine(h, 2 * E)
+    dev = eng.device
+    pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()})
+    eng.set_adjacency_edges(graphs, v, E)
+    a = eng.forward(torch.from_numpy(h0).to(dev), pack, T).cpu().numpy()
+    eng.set_adjacency(torch.from_numpy(A).to(dev))
+    d = eng.forward(torch.from_numpy(h0).to(dev), pack, T).cpu().numpy()
+    assert np.array_equal(a, d)
+    ref, _ = O.forward(A.astype(np.float64), h0.astype(np.float64), _f64(w), T, keep_cache=False)
+    assert np.abs(a - ref).max() <= FP32_TOL
+
+
+def test_generic_bf16_statistical():
+    b, v, h, C, T = 2, 150, 400, 4, 2
+    A, h0, w = _case(b, v, h, C, seed=12)
+    dhT = np.random.default_rng(6).standard_normal((b, v, h)).astype(np.float32)
+    ref, gref = _ref(A, h0, w, T, dhT)
+    got = _run(A, h0, w, T, "bf16", dhT=dhT)
+    assert _nrms(got["hT"], ref) <= 2e-2
+    for k in GRADS:
+        assert _nrms(got[k].reshape(gref[k].shape), gref[k]) <= 5e-2, k

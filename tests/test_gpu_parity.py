@@ -56,11 +56,12 @@ def _f64(w):
     return {k: x.astype(np.float64) for k, x in w.items()}
 
 
-def _run(A, h0, w, T, precision, use_bias=True, dhT=None, skip=True):
+def _run(A, h0, w, T, precision, use_bias=True, dhT=None, skip=True, generic=False):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, C, v, _ = A.shape
-    eng = PropagationEngine(h0.shape[-1], C, use_edge_bias=use_bias, precision=precision, skip_empty_channels=skip)
+    eng = PropagationEngine(h0.shape[-1], C, use_edge_bias=use_bias, precision=precision, skip_empty_channels=skip,
+                            force_generic=generic)
     dev = eng.device
     pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()})
     eng.set_adjacency(torch.from_numpy(np.ascontiguousarray(A)).to(dev))
@@ -298,10 +299,14 @@ def test_errors_are_raised_not_ignored():
         eng.forward(torch.zeros((2, 8, 128), device=eng.device), None, 1)
     with pytest.raises(ValueError):
         eng.set_adjacency(torch.zeros((2, 3, 8, 8), device=eng.device))
+    with pytest.raises(_lib.GGNNError):      # hidden outside 1..4096
+        PropagationEngine(5000, 4).dims(1, 1, 1)
+    with pytest.raises(_lib.GGNNError):      # C > 4096
+        PropagationEngine(128, 5000).dims(1, 1, 1)
     with pytest.raises(_lib.GGNNError):
-        PropagationEngine(100, 4).dims(1, 1, 1)
-    with pytest.raises(_lib.GGNNError):
-        eng.dims(1, 200, 1)
+        eng.dims(0, 20, 1)
+    PropagationEngine(100, 4).dims(1, 1, 1)  # any other hidden size / v: the general path
+    eng.dims(1, 200, 1)
 
 
 def test_drop_in_model_on_reference_dev_batches():
@@ -388,11 +393,11 @@ def test_dropout_masks_bit_exact(b, v, h, C, T, t):
     assert eng.dropout_mask("state", b, v, T, t, 1.0, seed).cpu().numpy().all()
 
 
-def _run_dropout(A, h0, w, T, precision, dr, dhT):
+def _run_dropout(A, h0, w, T, precision, dr, dhT, generic=False):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, C, v, _ = A.shape
-    eng = PropagationEngine(h0.shape[-1], C, precision=precision)
+    eng = PropagationEngine(h0.shape[-1], C, precision=precision, force_generic=generic)
     dev = eng.device
     pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()},
                             T=T, edge_keep=dr["edge_keep"], seed=dr["seed"])

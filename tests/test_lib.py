@@ -38,13 +38,17 @@ def test_dims_validation_and_sizes(lib):
     assert ws_t > ws_i > 0
     assert _lib.adjacency_bytes(d) >= 2 * 256 * 8 * 128 * 128 * 2
     assert _lib.weight_pack_bytes(d) >= 2 * 8 * 256 * 256 * 2
-    for bad, code in ((_lib.dims(1, 1, 100, 8, 5), -2), (_lib.dims(1, 129, 256, 8, 5), -2),
+    for bad, code in ((_lib.dims(1, 1, 5000, 8, 5), -2), (_lib.dims(1, 129, 256, 5000, 5), -2),
                       (_lib.dims(0, 10, 256, 8, 5), -1), (_lib.dims(1, 10, 256, 8, 0), -1)):
         rc = lib.ggnn_check_dims(__import__("ctypes").byref(bad))
         assert rc == code
         assert lib.ggnn_last_error().decode()
     with pytest.raises(_lib.GGNNError):
-        _lib.check_dims(_lib.dims(1, 1, 100, 8, 5))
+        _lib.check_dims(_lib.dims(1, 1, 5000, 8, 5))
+    # every other hidden size / vertex count is served by the general path
+    for ok in (_lib.dims(1, 1, 100, 8, 5), _lib.dims(2, 198, 400, 92, 5), _lib.dims(1, 129, 256, 8, 5)):
+        _lib.check_dims(ok)
+        assert _lib.workspace_bytes(ok, True) > _lib.workspace_bytes(ok, False) > 0
 
 
 def test_null_pointers_are_rejected_without_gpu(lib):
@@ -68,7 +72,8 @@ def test_dropout_dims_validation_and_sizes(lib):
     d2 = _lib.dims(256, 128, 256, 8, 5, edge_keep=0.9, state_keep=0.9, seed=3)
     d3 = _lib.dims(256, 128, 256, 8, 5, edge_keep=1.0, state_keep=0.9, seed=3)
     p1, p2 = _lib.weight_pack_bytes(d1), _lib.weight_pack_bytes(d2)
-    assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2)       # (T-1) extra masked copies of W and W^T
+    # (T-1) extra masked copies of W and W^T (hi + lo limbs) and of the general path's fp32 W
+    assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4)
     assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
     assert _lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True) == 5 * 8 * 256 * 256 * 4
     assert _lib.workspace_bytes(d2, False) == _lib.workspace_bytes(d1, False)
