@@ -75,6 +75,7 @@ GemmArgs gg_args() {
   a.zdiv = 1;
   a.Z = 1;
   a.alpha = 1.0f;
+  a.scA = a.scB = 1.0f;
   return a;
 }
 
@@ -85,7 +86,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
   const dim3 grid((unsigned)((a.N + 63) / 64), (unsigned)((a.M + 63) / 64), (unsigned)std::min(a.Z, 65535));
-  Prof p(kind, s);
+  Prof p(kind, s);  // (kind < 0: no record, the caller's own Prof scope covers it)
 #define GGL(A16_, AKC_, BKC_) hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_>), grid, dim3(256), 0, s, a)
   if (A16 && AKC && !BKC) GGL(true, true, false);
   else if (A16 && !AKC && !BKC) GGL(true, false, false);
@@ -170,7 +171,7 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     gt.B = P<float>(pack, PL.gWg); gt.sBq = H * 2 * H; gt.sBk = 2 * H; gt.sBn = 1;
     gt.D = P<float>(ws, L.g(t)); gt.sDm = 2 * H; gt.sDn = 1;
     gt.bias = P<float>(pack, PL.bg);
-    gt.tl = P<int>(pack, PL.two); gt.ts = 0;
+    gt.nterm = 2;
     gt.M = (int)N; gt.N = (int)(2 * H); gt.K = (int)H; gt.epi = GG_EPI_SIGMOID;
     if (int e = gg_launch<PREC>(gt, false, true, false, K_GRU_FWD, s)) return e;
     {
@@ -184,7 +185,7 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     cd.B = P<float>(pack, PL.gWc); cd.sBq = H * H; cd.sBk = H; cd.sBn = 1;
     cd.D = P<float>(ws, L.cc(t)); cd.sDm = H; cd.sDn = 1;
     cd.bias = P<float>(pack, PL.bc);
-    cd.tl = P<int>(pack, PL.two); cd.ts = 0;
+    cd.nterm = 2;
     cd.M = (int)N; cd.N = (int)H; cd.K = (int)H; cd.epi = GG_EPI_TANH;
     if (int e = gg_launch<PREC>(cd, false, true, false, K_GRU_FWD, s)) return e;
     {

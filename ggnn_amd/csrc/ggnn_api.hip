@@ -60,7 +60,7 @@ struct Prof {
   int idx = -1;
   hipStream_t s;
   Prof(int k, hipStream_t st) : s(st) {
-    if (g_prof.on && g_prof.used < g_prof.cap) {
+    if (k >= 0 && g_prof.on && g_prof.used < g_prof.cap) {
       idx = g_prof.used++;
       g_prof.kind[idx] = k;
       hipEventRecord(g_prof.ev[2 * idx], s);
@@ -143,7 +143,7 @@ size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 struct PackL {
   bool fast;
   size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, szW;
-  size_t gW, gszW, gWg, gWc, two, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc
+  size_t gW, gszW, gWg, gWc, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc
   long loW, loWg, loWc;  // element offset of the lo part from the hi part
   size_t wf(int t) const { return Wf + (size_t)t * szW; }
   size_t wt(int t) const { return WT + (size_t)t * szW; }
@@ -175,7 +175,6 @@ PackL pack_layout(const Cfg& c) {
   L.gW = o;   o += L.gszW * nW;
   L.gWg = o;  o += al(4 * H * H * 4);
   L.gWc = o;  o += al(2 * H * H * 4);
-  L.two = o;  o += al(3 * 4);  // the term list [2, 0, 1] of the general path's two-operand GRU products
   L.total = o;
   return L;
 }
@@ -791,7 +790,6 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
   copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
   copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
-  copy(nullptr, P<float>(pack, L.two), 3, 3);
   flush();
   LAUNCHCHK();
   return GGNN_OK;
@@ -1060,7 +1058,7 @@ int head_layout(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, H
   const size_t rows = (size_t)d->b * d->v, K = 2 * (size_t)d->h;
   size_t o = 0;
   for (int i = 0; i < nheads; ++i) {
-    if (heads[i].o < 1 || !heads[i].weight || !heads[i].bias)
+    if (heads[i].o < 1 || heads[i].o > HEAD_MAXO || !heads[i].weight || !heads[i].bias)
       return fail(GGNN_EINVAL, std::string(what) + ": bad head " + std::to_string(i));
     const size_t w = (size_t)heads[i].o;
     L->Wd[i] = o; o += al(K * w * 4);
@@ -1100,9 +1098,16 @@ int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nh
     float* Wd = P<float>(ws, L.Wd[i]);
     float* S = P<float>(ws, L.S[i]);
     hipLaunchKernelGGL(k_head_wdrop, dim3(grid1d((long)K * o)), dim3(256), 0, s, hd.weight, K, o, i, dr, Wd, S);
-    HeadLogitsP q{hT, h0, Wd, hd.bias, hd.probs, (int)rows, o, K, H};
-    hipLaunchKernelGGL(k_sgemm<HeadLogitsP>, dim3((o + 63) / 64, (unsigned)((rows + 63) / 64), 1), dim3(256), 0, s, q);
-    hipLaunchKernelGGL(k_head_softmax, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, hd.probs,
+    // z = [hT | h0] Wd + b on MFMA (split f16 limbs, fp32 accumulation): two
+    // terms, one per half of the concatenation
+    GemmArgs q = gg_args();
+    q.A = hT; q.A2 = h0; q.sAm = H; q.sAk = 1;
+    q.B = Wd; q.sBq = (long)H * o; q.sBk = o; q.sBn = 1;
+    q.D = hd.probs; q.sDm = o; q.sDn = 1;
+    q.bias = hd.bias;
+    q.nterm = 2; q.M = (int)rows; q.N = o; q.K = H;
+    if (int e = gg_launch<PREC_SPLIT>(q, false, true, false, -1, s)) return e;
+    hipLaunchKernelGGL(k_head_softmax, dim3((unsigned)std::min<long>(2048, (rows + 3) / 4)), dim3(256), 0, s, hd.probs,
                        loss ? hd.labels : (const float*)nullptr, rows, o, 1.0f / target_num, loss ? loss + i : nullptr);
   }
   LAUNCHCHK();
@@ -1134,16 +1139,38 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
     const ggnn_output_head& hd = heads[i];
     const int o = hd.o;
     float* dZ = P<float>(ws, L.dZ[i]);
-    hipLaunchKernelGGL(k_head_dz, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, hd.probs, hd.labels, rows, o,
-                       1.0f / target_num, d_loss, dZ);
-    HeadDxP q{dZ, P<const float>(ws, L.Wd[i]), dhT, dh0, (int)rows, K, o, H, i > 0};
-    hipLaunchKernelGGL(k_sgemm<HeadDxP>, dim3(K / 64 + (K % 64 != 0), (unsigned)((rows + 63) / 64), 1), dim3(256), 0, s,
-                       q);
-    HeadDwP w{hT, h0, dZ, P<const float>(ws, L.S[i]), hd.d_weight, K, o, H, rows};
-    const unsigned splits = (unsigned)std::max<long>(1, std::min<long>(64, rows / 256));
-    hipLaunchKernelGGL(k_sgemm<HeadDwP>, dim3((o + 63) / 64, (K + 63) / 64, splits), dim3(256), 0, s, w);
-    hipLaunchKernelGGL(k_colsum, dim3((o + 63) / 64, (unsigned)std::min<long>(256, rows)), dim3(64), 0, s, dZ, rows, o,
-                       hd.d_bias);
+    hipLaunchKernelGGL(k_head_dz, dim3((unsigned)std::min<long>(512, (rows + 3) / 4)), dim3(256), 0, s, hd.probs,
+                       hd.labels, rows, o, 1.0f / target_num, d_loss, dZ, hd.d_bias);
+    // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
+    // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
+    int ex = 0;
+    frexpf(target_num, &ex);
+    const float S = ldexpf(1.0f, std::max(-100, std::min(100, ex - 1)));
+    const float* Wd = P<const float>(ws, L.Wd[i]);
+    // (hidden a multiple of 64: each product in one launch with the output /
+    // operand split at H; otherwise one launch per half)
+    const bool one = H % 64 == 0;
+    for (int half = 0; half < (one ? 1 : 2); ++half) {
+      // [dhT | dh0] (+)= dZ Wd^T  (B(k=j, n=c) = Wd[c][j])
+      GemmArgs q = gg_args();
+      q.A = dZ; q.sAm = o; q.sAk = 1; q.scA = S; q.alpha = 1.0f / S;
+      q.B = Wd + (long)half * H * o; q.sBk = 1; q.sBn = o;
+      q.D = half ? dh0 : dhT; q.sDm = H; q.sDn = 1; q.mode = i > 0 ? GG_ADD : GG_STORE;
+      q.M = (int)rows; q.N = one ? 2 * H : H; q.K = o;
+      if (one) { q.D2 = dh0; q.Nsplit = H; }
+      if (int e = gg_launch<PREC_SPLIT>(q, false, true, true, -1, s)) return e;
+      // dW[rows of the half] += S_drop * ([hT | h0]^T dZ): split-K over node rows, atomics
+      const long KC = std::max<long>(256, ((rows + 47) / 48 + 31) & ~31L);
+      GemmArgs w = gg_args();
+      w.A = half ? h0 : hT; w.sAp = KC * H; w.sAm = 1; w.sAk = H;
+      w.B = dZ; w.sBp = KC * o; w.sBk = o; w.sBn = 1; w.scB = S; w.alpha = 1.0f / S;
+      w.D = hd.d_weight + (long)half * H * o; w.sDm = o; w.sDn = 1; w.mode = GG_ATOMIC;
+      w.E = P<const float>(ws, L.S[i]) + (long)half * H * o;
+      w.Z = (int)((rows + KC - 1) / KC); w.M = one ? 2 * H : H; w.N = o; w.K = (int)KC; w.Ktot = rows; w.sKp = KC;
+      if (one) { w.Am2 = h0; w.Msplit = H; }
+      if (int e = gg_launch<PREC_SPLIT>(w, false, false, false, -1, s)) return e;
+    }
+
   }
   LAUNCHCHK();
   return GGNN_OK;

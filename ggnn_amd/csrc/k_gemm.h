@@ -30,9 +30,13 @@
 
 struct GemmArgs {
   const void* A;        // fp32, or 16-bit exact limbs (A16)
+  const void* A2;       // if set: the A base of the terms with q == 1 (two separate operands, e.g. [hT | h0])
   const float* B;
   float* D;
   const float* bias;    // [N] at zp*sbp + zq*sbq, or null
+  const float* E;       // if set: D's element-wise multiplier (same offsets as D), e.g. a dropout scale
+  float scA, scB;       // exact power-of-two operand scales applied before the limb split (small
+                        // operands stay in the f16 normal range); alpha undoes them
   long sAp, sAq, sAm, sAk;
   long sBp, sBq, sBk, sBn;
   long sDz, sDp, sDq, sDm, sDn;
@@ -40,14 +44,23 @@ struct GemmArgs {
   // z -> (zp, zq) = (z / zdiv, z % zdiv); z is skipped when zmask && !zmask[z]
   int zdiv;
   const unsigned char* zmask;
-  // terms of z: tl == null: one term (zp, zq); else nt = tl[z*ts] terms
-  // (zp, tl[z*ts + 1 + e]) (a count-prefixed list, e.g. a graph's channels)
+  // terms of z: tl == null: nterm terms (zp, zq + e) (nterm 0 = 1); else
+  // nt = tl[z*ts] terms (zp, tl[z*ts + 1 + e]) (a count-prefixed list, e.g. a
+  // graph's channels)
   const int* tl;
   long ts;
+  int nterm;
   int Z, M, N, K;       // per-term K; term k range [p*sKp, p*sKp + K) clipped to Ktot
   long Ktot, sKp;
   float alpha;
   int epi, mode;
+  // row / column splits of one product over two buffers (Msplit, Nsplit
+  // multiples of 64; 0 = none): A rows m >= Msplit come from Am2 (row
+  // m - Msplit), outputs n >= Nsplit go to D2 (column n - Nsplit)
+  const void* Am2;
+  int Msplit;
+  float* D2;
+  int Nsplit;
 };
 
 namespace gg {
@@ -55,6 +68,114 @@ constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
 constexpr int PITCH = 80;                  // bytes per LDS row: 32 limbs + 16 B pad
 constexpr int TILE = 64 * PITCH;           // one [64][32] limb image
 }  // namespace gg
+
+// One operand's share of a [64 rows][32 k] stage per thread (8 values), rows
+// = m (A) or n (B), element (row, k) at base + row*sR + k*sK:
+//   KC (k contiguous): row tid>>2, k (tid&3)*8 .. +7    -> 16-byte loads
+//   else (rows contiguous): rows 2(tid&31) and +1, k (tid>>5)*4 .. +3
+//                           -> 8-byte loads per k (lanes cover 64 rows: 256 B)
+// with a scalar, bounds-checked fallback on edge tiles / unaligned operands.
+template <bool KC, bool U16, bool F16L>
+DEV void gg_load(float* x, const void* P, long base, long sR, long sK, int r0, int R, int kk0, int K, long kg0,
+                 long Ktot, float sc, int tid) {
+  auto val = [&](long off) -> float {
+    if constexpr (U16) return from_limb<F16L>(((const u16*)P)[off]);
+    else return ((const float*)P)[off] * sc;
+  };
+  if constexpr (KC) {
+    const int row = r0 + (tid >> 2), kq = (tid & 3) * 8;
+    const long off = base + (long)row * sR + (long)(kk0 + kq) * sK;
+    const bool full = row < R && kk0 + kq + 7 < K && kg0 + kq + 7 < Ktot && sK == 1;
+    if constexpr (U16) {
+      const u16* p = (const u16*)P + off;
+      if (full && ((uintptr_t)p & 15) == 0) {
+        const uint4 w = *(const uint4*)p;
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[2 * j] = from_limb<F16L>((u16)(ws[j] & 0xFFFF));
+          x[2 * j + 1] = from_limb<F16L>((u16)(ws[j] >> 16));
+        }
+        return;
+      }
+    } else {
+      const float* p = (const float*)P + off;
+      if (full && ((uintptr_t)p & 15) == 0) {
+        const float4 a0 = *(const float4*)p, a1 = *(const float4*)(p + 4);
+        x[0] = a0.x * sc; x[1] = a0.y * sc; x[2] = a0.z * sc; x[3] = a0.w * sc;
+        x[4] = a1.x * sc; x[5] = a1.y * sc; x[6] = a1.z * sc; x[7] = a1.w * sc;
+        return;
+      }
+      if (full && ((uintptr_t)p & 7) == 0) {  // rows of an odd number of float pairs (e.g. o = 150)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 w = *(const float2*)(p + 2 * j);
+          x[2 * j] = w.x * sc;
+          x[2 * j + 1] = w.y * sc;
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = row < R && kk0 + kq + j < K && kg0 + kq + j < Ktot;
+      x[j] = ok ? val(base + (long)row * sR + (long)(kk0 + kq + j) * sK) : 0.f;
+    }
+  } else {
+    const int row = r0 + 2 * (tid & 31), kq = (tid >> 5) * 4;
+    const bool full = row + 1 < R && kk0 + kq + 3 < K && kg0 + kq + 3 < Ktot && sR == 1;
+    const long off = base + (long)row + (long)(kk0 + kq) * sK;
+    if constexpr (U16) {
+      const u16* p = (const u16*)P + off;
+      if (full && ((uintptr_t)p & 3) == 0 && (sK & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t w = *(const uint32_t*)(p + j * sK);
+          x[j] = from_limb<F16L>((u16)(w & 0xFFFF));
+          x[4 + j] = from_limb<F16L>((u16)(w >> 16));
+        }
+        return;
+      }
+    } else {
+      const float* p = (const float*)P + off;
+      if (full && ((uintptr_t)p & 7) == 0 && (sK & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 w = *(const float2*)(p + j * sK);
+          x[j] = w.x * sc;
+          x[4 + j] = w.y * sc;
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = row + r < R && kk0 + kq + j < K && kg0 + kq + j < Ktot;
+        x[4 * r + j] = ok ? val(base + (long)(row + r) * sR + (long)(kk0 + kq + j) * sK) : 0.f;
+      }
+  }
+}
+// the same share into the [row][k] limb image(s) (hi; lo when LO)
+template <bool KC, bool F16, bool LO>
+DEV void gg_store(char* hi, char* lo, const float* x, int tid) {
+  using namespace gg;
+  if constexpr (KC) {
+    const int o = (tid >> 2) * PITCH + (tid & 3) * 16;
+    st16(hi + o, pk8<F16>(x));
+    if constexpr (LO) st16(lo + o, pk8_lo<true>(x));
+  } else {
+    const int row = 2 * (tid & 31), kq = (tid >> 5) * 4;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int o = (row + r) * PITCH + kq * 2;
+      const float* y = x + 4 * r;
+      *(uint2*)(hi + o) = make_uint2(pk<F16>(y[0], y[1]), pk<F16>(y[2], y[3]));
+      if constexpr (LO) *(uint2*)(lo + o) = make_uint2(pk_lo<true>(y[0], y[1]), pk_lo<true>(y[2], y[3]));
+    }
+  }
+}
 
 template <int PREC, bool A16, bool AKC, bool BKC>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
@@ -70,11 +191,11 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   for (int z = blockIdx.z; z < a.Z; z += gridDim.z) {
     if (a.zmask && !a.zmask[z]) continue;
     const int zp = z / a.zdiv, zq = z % a.zdiv;
-    const int nt = a.tl ? a.tl[(long)z * a.ts] : 1;
+    const int nt = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
     const int nst = nt * kc;
     auto term = [&](int e, int& p, int& q) {
       p = zp;
-      q = a.tl ? a.tl[(long)z * a.ts + 1 + e] : zq;
+      q = a.tl ? a.tl[(long)z * a.ts + 1 + e] : zq + e;
     };
 
     // ---- global -> registers: this thread's 8 A values and 8 B values of a stage
@@ -84,71 +205,23 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
       term(st / kc, p, q);
       const int kk0 = (st % kc) * BK;
       const long kg0 = (long)p * a.sKp + kk0;  // global k of the slice's first column
-      // A: AKC -> (row m = tid>>2, 8 k at (tid&3)*8); else (k = tid>>3, 8 m at (tid&7)*8)
-      {
-        const int mi = AKC ? (tid >> 2) : (tid & 7) * 8;
-        const int ki = AKC ? (tid & 3) * 8 : (tid >> 3);
-        const long base = p * a.sAp + q * a.sAq;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int m = m0 + mi + (AKC ? 0 : j), kk = kk0 + ki + (AKC ? j : 0);
-          const long kg = kg0 + ki + (AKC ? j : 0);
-          float x = 0.f;
-          if (m < a.M && kk < a.K && kg < a.Ktot) {
-            const long off = base + m * a.sAm + kk * a.sAk;
-            if constexpr (A16) x = from_limb<F16>(((const u16*)a.A)[off]);
-            else x = ((const float*)a.A)[off];
-          }
-          ra[j] = x;
-        }
-      }
-      // B: BKC -> (col n = tid>>2, 8 k at (tid&3)*8); else (k = tid>>3, 8 n at (tid&7)*8)
-      {
-        const int ni = BKC ? (tid >> 2) : (tid & 7) * 8;
-        const int ki = BKC ? (tid & 3) * 8 : (tid >> 3);
-        const long base = p * a.sBp + q * a.sBq;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int n = n0 + ni + (BKC ? 0 : j), kk = kk0 + ki + (BKC ? j : 0);
-          const long kg = kg0 + ki + (BKC ? j : 0);
-          float x = 0.f;
-          if (n < a.N && kk < a.K && kg < a.Ktot) x = a.B[base + n * a.sBn + kk * a.sBk];
-          rb[j] = x;
-        }
-      }
+      const bool second = a.A2 && q == 1;
+      const bool lowm = a.Msplit && m0 >= a.Msplit;  // block-uniform row split
+      const void* Ab = lowm ? a.Am2 : second ? a.A2 : a.A;
+      const int am0 = lowm ? m0 - a.Msplit : m0;
+      const int aM = lowm ? a.M - a.Msplit : a.Msplit ? a.Msplit : a.M;
+      const long abase = p * a.sAp + (second ? 0 : q * a.sAq);
+      if constexpr (A16)
+        gg_load<AKC, true, F16>(ra, Ab, abase, a.sAm, a.sAk, am0, aM, kk0, a.K, kg0, a.Ktot, 1.0f, tid);
+      else
+        gg_load<AKC, false, F16>(ra, Ab, abase, a.sAm, a.sAk, am0, aM, kk0, a.K, kg0, a.Ktot, a.scA, tid);
+      gg_load<BKC, false, F16>(rb, a.B, p * a.sBp + q * a.sBq, a.sBn, a.sBk, n0, a.N, kk0, a.K, kg0, a.Ktot, a.scB, tid);
     };
     // ---- registers -> LDS limb images ([row][k], k contiguous)
     auto store = [&](int buf) {
       char* ah = smem + buf * 4 * TILE;
-      char* al = ah + TILE;
-      char* bh = ah + 2 * TILE;
-      char* bl = ah + 3 * TILE;
-      if constexpr (AKC) {
-        const int o = (tid >> 2) * PITCH + (tid & 3) * 16;
-        st16(ah + o, pk8<F16>(ra));
-        if constexpr (SPLIT && !A16) st16(al + o, pk8_lo<true>(ra));
-      } else {
-        const int k = tid >> 3, mb = (tid & 7) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int o = (mb + j) * PITCH + k * 2;
-          *(u16*)(ah + o) = to_limb<F16>(ra[j]);
-          if constexpr (SPLIT && !A16) *(u16*)(al + o) = to_limb<true>(lo_part<true>(ra[j]));
-        }
-      }
-      if constexpr (BKC) {
-        const int o = (tid >> 2) * PITCH + (tid & 3) * 16;
-        st16(bh + o, pk8<F16>(rb));
-        if constexpr (SPLIT) st16(bl + o, pk8_lo<true>(rb));
-      } else {
-        const int k = tid >> 3, nb = (tid & 7) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int o = (nb + j) * PITCH + k * 2;
-          *(u16*)(bh + o) = to_limb<F16>(rb[j]);
-          if constexpr (SPLIT) *(u16*)(bl + o) = to_limb<true>(lo_part<true>(rb[j]));
-        }
-      }
+      gg_store<AKC, F16, SPLIT && !A16>(ah, ah + TILE, ra, tid);
+      gg_store<BKC, F16, SPLIT>(ah + 2 * TILE, ah + 3 * TILE, rb, tid);
     };
 
     f32x16 acc = splat(0.f);
@@ -194,7 +267,10 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
         float x = a.alpha * acc[r] + bn;
         if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
         else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-        float* d = a.D + dbase + (long)m * a.sDm + (long)n * a.sDn;
+        const bool hi_n = a.Nsplit && n >= a.Nsplit;
+        const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+        if (a.E) x *= a.E[doff];
+        float* d = (hi_n ? a.D2 : a.D) + doff;
         if (a.mode == GG_ATOMIC) atomicAdd(d, x);
         else if (a.mode == GG_ADD) *d += x;
         else *d = x;

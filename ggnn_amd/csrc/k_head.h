@@ -204,13 +204,14 @@ struct HeadDwP {
   DEV void store(int m, int n, float v) const { atomicAdd(dW + (long)m * N + n, v * S[(long)m * N + n]); }
 };
 
-// in place z -> p = softmax(z) per row (one wave per row), loss += -sum y log p / num
+// in place z -> p = softmax(z) per row (one wave per row, rows grid-strided
+// over a few hundred blocks), loss += -sum y log p / num (one atomic per block:
+// one per 4 rows serialised 8192 same-address atomics at b*v = 32768)
 __global__ void __launch_bounds__(256) k_head_softmax(float* __restrict__ zp, const float* __restrict__ y, long rows,
                                                       int o, float inv_num, float* __restrict__ loss) {
   const int lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   float term = 0.f;
-  if (r < rows) {
+  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) {
     float* z = zp + r * o;
     float mx = -INFINITY;
     for (int j = lane; j < o; j += 64) mx = fmaxf(mx, z[j]);
@@ -236,18 +237,40 @@ __global__ void __launch_bounds__(256) k_head_softmax(float* __restrict__ zp, co
   }
 }
 
-// dZ = g * (p * sum(y) - y) / num per row (d/dz of -sum y log softmax(z))
+// dZ = g * (p * sum(y) - y) / num per row (d/dz of -sum y log softmax(z)), and
+// the bias gradient db[j] += sum_r dZ[r][j]: column partials in registers
+// (lane l owns columns l + 64i, o <= HEAD_MAXO), summed over the block's waves
+// in LDS, one global atomic per column per block
+#define HEAD_MAXO 1024
 __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, const float* __restrict__ y, long rows,
                                                  int o, float inv_num, const float* __restrict__ dloss,
-                                                 float* __restrict__ dZ) {
-  const int lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
+                                                 float* __restrict__ dZ, float* __restrict__ db) {
+  constexpr int NI = HEAD_MAXO / 64;
+  __shared__ float cs[4][HEAD_MAXO];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float g = (dloss ? *dloss : 1.0f) * inv_num;
-  float sy = 0.f;
-  for (int j = lane; j < o; j += 64) sy += y[r * o + j];
-  for (int s = 32; s >= 1; s >>= 1) sy += __shfl_xor(sy, s);
-  for (int j = lane; j < o; j += 64) dZ[r * o + j] = g * (p[r * o + j] * sy - y[r * o + j]);
+  float part[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) part[i] = 0.f;
+  for (long r = (long)blockIdx.x * 4 + w; r < rows; r += (long)gridDim.x * 4) {
+    float sy = 0.f;
+    for (int j = lane; j < o; j += 64) sy += y[r * o + j];
+    for (int s = 32; s >= 1; s >>= 1) sy += __shfl_xor(sy, s);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = lane + 64 * i;
+      if (j < o) {
+        const float d = g * (p[r * o + j] * sy - y[r * o + j]);
+        dZ[r * o + j] = d;
+        part[i] += d;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    if (lane + 64 * i < o) cs[w][lane + 64 * i] = part[i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < o; j += 256) atomicAdd(db + j, cs[0][j] + cs[1][j] + cs[2][j] + cs[3][j]);
 }
 
 // db[j] = sum_r dZ[r][j] (2D grid: blockIdx.y strides the rows; atomics)

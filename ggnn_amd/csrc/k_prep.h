@@ -362,10 +362,6 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     ((float*)J.out)[q] = x;
     return;
   }
-  if (J.copy == 3) {  // the general path's two-term list [2, 0, 1]
-    ((int*)J.out)[q] = q == 0 ? 2 : (int)q - 1;
-    return;
-  }
   const int per = (J.N / 32) * (J.K / 16) * 64;  // fragment-lanes per matrix
   const int mat = (int)(q / per), r = (int)(q % per);
   const float* Sb = J.S + J.sS * mat;

@@ -242,7 +242,7 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
 typedef struct ggnn_output_head {
   const float* weight; /* MLP_W_layer0 [2h][o] */
   const float* bias;   /* MLP_b_layer0 [o] */
-  int32_t o;
+  int32_t o;           /* output width, 1..1024 */
   const float* labels; /* [b][v][o] targets, or NULL (no loss) */
   float* probs;        /* [b][v][o] out */
   float* d_weight;     /* [2h][o] (backward; overwritten) */
