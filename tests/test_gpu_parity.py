@@ -597,15 +597,20 @@ def test_edge_dropout_long_unroll_packs_in_several_launches():
     assert np.abs(got["hT"] - ref).max() <= FP32_TOL
 
 
-def _tree_adjacency(b, v, E, seed):
+def _tree_adjacency(b, v, E, seed, zipf=False, first_empty=True):
     """Dependency-tree-shaped graphs (graph_to_adj_mat_bd, chem_tensorflow_dense.py:65-83)
     with E labels: most of the 2E channels of a graph are empty, as in the real
-    btb data (~30-38 of 92 non-empty).  Graph 0 has no edge at all."""
+    btb data (~30-38 of 92 non-empty).  zipf: label k drawn with
+    P ~ 1/k (a few labels dominate a treebank).  first_empty: graph 0 has no
+    edge at all."""
     rng = np.random.default_rng(seed)
     A = np.zeros((b, 2 * E, v, v), np.float32)
-    for g in range(1, b):
+    pz = 1.0 / np.arange(1, E + 1)
+    pz /= pz.sum()
+    for g in range(1 if first_empty else 0, b):
         n = int(rng.integers(v // 2, v + 1))
-        edges = [(int(rng.integers(0, i)), int(rng.integers(1, E + 1)), i) for i in range(1, n)]
+        lab = (lambda: int(rng.choice(E, p=pz)) + 1) if zipf else (lambda: int(rng.integers(1, E + 1)))
+        edges = [(int(rng.integers(0, i)), lab(), i) for i in range(1, n)]
         A[g] = O.graph_to_adj_mat_bd(edges, v, E, dtype=np.float32)
     return A
 
@@ -644,3 +649,34 @@ def test_empty_channel_skipping_is_bit_identical(b, v, h, E, T, precision):
         assert np.abs(skip["hT"] - ref).max() <= FP32_TOL
         for k in GRADS:
             assert _nmax(skip[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
+@pytest.mark.parametrize("v,parity_bias", [(30, False), (30, True), (100, False)])
+def test_bf16_within_north_star_on_dependency_trees(v, parity_bias):
+    """north_star: bf16 outputs within 1e-2 of the reference.  On the graphs the
+    reference trains on (dependency trees, E = 46 labels -> C = 92 channels,
+    in-degree ~2 per node) the bf16 mode meets it as written, forward and
+    gradients, at T = 5.  (On SURVEY §8d's dense Bernoulli(0.1) synthetic
+    adjacency, in-degree ~100, X reaches rms ~2 and the GRU saturates: there
+    rounding the WEIGHTS alone to bf16 moves the float64 output by 3.9e-2
+    normalised RMS at T = 5 (oracle emulation), so no bf16-weight kernel can be
+    within 1e-2; test_forward_bf16_matches_rounding_emulation pins the engine
+    to that emulation instead.)"""
+    b, h, E, T = 8, 256, 46, 5
+    C = 2 * E
+    A = _tree_adjacency(b, v, E, seed=v + int(parity_bias), zipf=True, first_empty=False)
+    rng = np.random.default_rng(v)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, C, seed=3, parity_bias=parity_bias)
+    dhT = rng.standard_normal((b, v, h)).astype(np.float32)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run(A, h0, w, T, "bf16", dhT=dhT)
+    errs = {"hT_nrms": _nrms(got["hT"], ref), "hT_max": float(np.abs(got["hT"] - ref).max())}
+    for k in GRADS:
+        errs[k] = _nrms(got[k].reshape(gref[k].shape), gref[k])
+    print("bf16 on dependency trees:", errs)
+    assert errs["hT_nrms"] <= BF16_RMS_TOL and errs["hT_max"] <= BF16_RMS_TOL
+    for k in GRADS:
+        assert errs[k] <= BF16_RMS_TOL, (k, errs[k])
