@@ -327,6 +327,48 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
     return res
 
 
+def end_to_end_side(dev, n_train=1000, n_valid=200, hidden=None, steps_note=""):
+    """Side measurement: the reference's own metric,
+    instance_per_sec of run_epoch (chem_tensorflow.py:528-667, :660) -- host
+    batching in a background thread, train step (front-end, propagation,
+    heads, clip + Adam) or eval forward, host LAS/UAS per batch -- with the
+    reference's default params (hidden_size 400, num_timesteps 4, batch_size
+    20, embeddings 80/50/100/80) on a synthetic treebank of WSJ-dev-like
+    sentence lengths (ggnn_amd.batching.synthetic_treebank; the treebank
+    itself is not distributed).  One warm-up epoch, then one timed train and
+    one timed valid epoch."""
+    from ggnn_amd.batching import synthetic_treebank
+    from ggnn_amd.model import DenseGGNNChemModel
+    raw = synthetic_treebank(n_train + n_valid, seed=2)
+    params = {"compact_adjacency": True}
+    if hidden:
+        params["hidden_size"] = hidden
+    m = DenseGGNNChemModel(num_edge_types=46, output_size_edges=12, pos_size=46, vocab_size=39549, params=params,
+                           seed=0, device=dev)
+    train = m.process_raw_graphs(raw[:n_train], True)
+    valid = m.process_raw_graphs(raw[n_train:], False)
+    m.run_epoch("warm-up", train, True)
+    tr = m.run_epoch("train", train, True)
+    va = m.run_epoch("valid", valid, False)
+    # README.md:25-43's sample run: --restrict_data 100 (100 sentences per
+    # split: small bucketed batches, avg 3.85 / 4.35 graphs), epoch 1
+    small = m.process_raw_graphs(raw[:100], True)
+    small_v = m.process_raw_graphs(raw[n_train:n_train + 100], False)
+    tr100 = m.run_epoch("train r100", small, True)
+    va100 = m.run_epoch("valid r100", small_v, False)
+    return {"params": {k: m.params[k] for k in ("hidden_size", "num_timesteps", "batch_size")},
+            "train_instances_per_sec": tr[3], "train_steps": tr[4], "train_loss": tr[0],
+            "valid_instances_per_sec": va[3], "valid_las": va[5], "valid_uas": va[6],
+            "sentences": {"train": n_train, "valid": n_valid},
+            "restrict_data_100": {"train_instances_per_sec": tr100[3], "train_steps": tr100[4],
+                                  "avg_train_batch": 100 / max(tr100[4], 1),
+                                  "valid_instances_per_sec": va100[3], "valid_steps": va100[4],
+                                  "reference_readme": {"train_instances_per_sec": 13.91,
+                                                       "valid_instances_per_sec": 31.51,
+                                                       "hardware": "unstated (BASELINE.md §1)"}},
+            "note": "the reference's run_epoch metric (host batching + LAS/UAS included), not the hot-path value"}
+
+
 def load_ceilings():
     """Library MFMA / copy ceilings measured on the box (tools/ceilings.py)."""
     p = os.path.join(ROOT, "profiles", "ceilings.json")
@@ -499,6 +541,7 @@ def main():
     bf16 = (precision_side(dev, "bf16", A_d, h0_d, w_d, dhT, b, v, h, C, T)
             if rank == 0 and not args.no_side and args.precision != "bf16" else None)
     real = real_density_side(dev) if rank == 0 and not args.no_side else None
+    e2e = end_to_end_side(dev) if rank == 0 and not args.no_side else None
 
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]
@@ -537,6 +580,7 @@ def main():
             "callers": callers,
             "bf16_mode": bf16,
             "real_density_c92": real,
+            "end_to_end_run_epoch": e2e,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_reps)

@@ -54,6 +54,72 @@ def target_to_adj_mat(target, max_n_vertices, num_edge_types, output_size, tie_f
     return amat
 
 
+class ThreadedIterator:
+    """Builds the next feed dicts in a background thread (utils.py:17-37): the
+    host batching overlaps the GPU step.  Elements must not be None; an
+    exception in the producer is re-raised in the consumer."""
+
+    _END = object()
+
+    def __init__(self, original_iterator, max_queue_size: int = 2):
+        import queue
+        import threading
+        self._queue = queue.Queue(maxsize=max_queue_size)
+        self._thread = threading.Thread(target=self._worker, args=(original_iterator,), daemon=True)
+        self._thread.start()
+
+    def _worker(self, it):
+        try:
+            for element in it:
+                assert element is not None, "iterator elements must not be None"
+                self._queue.put(element, block=True)
+        except BaseException as e:  # pragma: no cover - surfaced in __iter__
+            self._queue.put(e, block=True)
+            return
+        self._queue.put(self._END, block=True)
+
+    def __iter__(self):
+        while True:
+            x = self._queue.get(block=True)
+            if x is self._END:
+                break
+            if isinstance(x, BaseException):
+                raise x
+            yield x
+        self._thread.join()
+
+
+def synthetic_treebank(n_sentences, num_edge_types=46, output_size_edges=12, pos_size=46, vocab_size=39549,
+                       max_nodes=119, seed=0):
+    """Raw btb examples in the reference's JSON layout (keys as the parser
+    writes them, parser/to_graph.py; read by process_raw_graphs): sentence
+    lengths around the WSJ dev set's (mean ~25 nodes incl. ROOT, max 119;
+    SURVEY App. B), one input edge [head, label, dependent] per word with
+    Zipf-distributed labels 1..E-1, one target [head, label] per word.  For
+    benchmarks and tests only: the treebank itself is not distributed."""
+    rng = np.random.default_rng(seed)
+    E = int(num_edge_types)
+    pz = 1.0 / np.arange(1, E)
+    pz /= pz.sum()
+    out = []
+    for s in range(int(n_sentences)):
+        n = int(np.clip(round(rng.gamma(4.0, 6.0)), 3, max_nodes))
+        heads = [int(rng.integers(0, n)) for _ in range(1, n)]
+        heads = [h if h != i + 1 else 0 for i, h in enumerate(heads)]
+        graph = [[heads[i - 1], int(rng.choice(E - 1, p=pz)) + 1, i] for i in range(1, n)]
+        pos = [0] + [int(x) for x in rng.integers(1, pos_size, n - 1)]
+        out.append({
+            "graph": graph,
+            "targets": [[int(rng.integers(0, n)), int(rng.integers(1, output_size_edges + 1))] for _ in range(1, n)],
+            "node_features": pos,
+            "node_features_target": pos,
+            "words_index": [0] + [int(x) for x in rng.integers(1, vocab_size, n - 1)],
+            "raw_sentence": "",
+            "id": "%05d" % s,
+        })
+    return out
+
+
 class BtbBatching:
     """Mixin with the reference's btb batching API.  Requires the attributes
     the reference reads from ``self``: ``params`` (batch_size, output_size,

@@ -30,12 +30,14 @@ carry the autograd graph around the call.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
 from . import checkpoint as _ckpt
 from . import evaluation as _eval
-from .batching import BtbBatching
+from .batching import BtbBatching, ThreadedIterator
 from .engine import PropagationEngine
 from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
 from .optim import ClipAdam
@@ -395,6 +397,12 @@ class DenseGGNNChemModel(BtbBatching):
                     self.placeholders.pop(k, None)
                 else:
                     self.placeholders[k] = v
+        return self._score_batch()[:3]
+
+    def _score_batch(self):
+        """Host LAS/UAS of the staged batch from the last build_loss() (the
+        heads' probabilities are the only device tensors fetched).  Returns
+        (las, uas, label_acc, labels, probs, mask, labels_e, probs_e, mask_e)."""
         ph = self.placeholders
         b = int(ph["num_graphs"])
         v = int(ph["num_vertices"])
@@ -403,6 +411,68 @@ class DenseGGNNChemModel(BtbBatching):
         probs_e = self.ops["computed_values_edges"].detach().cpu().numpy()
         mask = np.asarray(ph["node_mask"], np.float32).reshape(b, v * o)
         mask_e = np.asarray(ph["node_mask_edges"], np.float32).reshape(b, v * oe)
-        return _eval.batch_las_uas(np.asarray(ph["target_values_head"], np.float32).reshape(b, v * o), probs, v, mask,
-                                   np.asarray(ph["target_values_edges"], np.float32).reshape(b, v * oe), probs_e,
-                                   mask_e, o, oe)
+        labels = np.asarray(ph["target_values_head"], np.float32).reshape(b, v * o)
+        labels_e = np.asarray(ph["target_values_edges"], np.float32).reshape(b, v * oe)
+        las, uas, uas_e = _eval.batch_las_uas(labels, probs, v, mask, labels_e, probs_e, mask_e, o, oe)
+        return las, uas, uas_e, labels, probs, mask, labels_e, probs_e, mask_e
+
+    # the reference's per-task "chemical accuracy" normalisers (chem_tensorflow.py:529-531)
+    CHEMICAL_ACCURACIES = np.array([0.066513725, 0.012235489, 0.071939046, 0.033730778, 0.033486113, 0.004278493,
+                                    0.001330901, 0.004165489, 0.004128926, 0.00409976, 0.004527465, 0.012292586,
+                                    0.037467458])
+
+    def run_epoch(self, epoch_name: str, data, is_training: bool, start_step: int = 0, verbose: bool = False):
+        """One pass over ``data`` (the output of process_raw_graphs), as
+        chem_tensorflow.py:528-667: minibatches built in a background thread
+        (ThreadedIterator, max_queue_size 5), a training step (is_training) or a
+        dropout-free forward per batch, host LAS/UAS from the heads'
+        probabilities.  Returns the reference's tuple (loss, accuracies,
+        error_ratios, instance_per_sec, steps, acc_las, acc_uas, all_labels,
+        all_computed_values, all_num_vertices, all_masks, all_ids, all_adj_m,
+        all_labels_e, all_computed_values_e, all_masks_e, acc_uas_e); for btb the
+        task "accuracy" is the task loss (chem_tensorflow.py:411).
+
+        Fetch diet: the reference's sess.run fetches 21 tensors per batch,
+        among them the dense [b, 2E, v, v] adjacency, the final node states and
+        the whole word-embedding table (:560-593); here only the loss and the
+        two heads' probabilities leave the device."""
+        loss = 0.0
+        accuracies = []
+        processed, steps = 0, 0
+        acc_las = acc_uas = acc_uas_e = 0.0
+        lists = {k: [] for k in ("labels", "cv", "nv", "mask", "ids", "adj", "labels_e", "cv_e", "mask_e")}
+        start = time.time()
+        for step, feed in enumerate(ThreadedIterator(self.make_minibatch_iterator(data, is_training),
+                                                     max_queue_size=5)):
+            b = int(feed["num_graphs"])
+            processed += b
+            if is_training:
+                feed["out_layer_dropout_keep_prob"] = self.params["out_layer_dropout_keep_prob"]
+                batch_loss = float(self.train_step(feed).detach())
+            else:
+                feed["out_layer_dropout_keep_prob"] = 1.0
+                self.feed(feed)
+                with torch.no_grad():
+                    batch_loss = float(self.build_loss())
+            las, uas, uas_e, labels, cv, mask, labels_e, cv_e, mask_e = self._score_batch()
+            loss += batch_loss * b
+            accuracies.append(np.array([batch_loss] * len(self.params["task_ids"])) * b)
+            acc_las += las * b
+            acc_uas += uas * b
+            acc_uas_e += uas_e * b
+            if verbose:
+                print("Running %s, batch %i (has %i graphs). Loss so far: %.4f" % (
+                    epoch_name, step, b, loss / processed), end="\r")
+            steps += 1
+            for k, x in (("labels", labels), ("cv", cv), ("nv", int(feed["num_vertices"])), ("mask", mask),
+                         ("ids", feed.get("sentences_id")), ("adj", feed.get("adjacency_matrix")),
+                         ("labels_e", labels_e), ("cv_e", cv_e), ("mask_e", mask_e)):
+                lists[k].append(x)
+        processed = max(processed, 1)
+        accuracies = np.sum(accuracies, axis=0) / processed
+        loss = loss / processed
+        error_ratios = accuracies / self.CHEMICAL_ACCURACIES[self.params["task_ids"]]
+        instance_per_sec = processed / (time.time() - start)
+        return (loss, accuracies, error_ratios, instance_per_sec, steps, acc_las / processed, acc_uas / processed,
+                lists["labels"], lists["cv"], lists["nv"], lists["mask"], lists["ids"], lists["adj"], lists["labels_e"],
+                lists["cv_e"], lists["mask_e"], acc_uas_e / processed)

@@ -76,3 +76,33 @@ def test_empty_graph_is_skipped_and_buckets():
     assert steps == [0] and sizes[0] == 4            # max node id 2 -> bucket 4
     fd = next(m.make_minibatch_iterator((bucketed, sizes, steps), False))
     assert fd["adjacency_matrix"][0].shape == (6, 4, 4) and fd["num_graphs"] == 1
+
+
+def test_threaded_iterator_and_synthetic_treebank():
+    """ThreadedIterator (utils.py:17-37) preserves order and surfaces producer
+    errors; the synthetic treebank (bench / e2e tests) goes through the
+    reference's batching unchanged."""
+    from ggnn_amd.batching import ThreadedIterator, synthetic_treebank
+    assert list(ThreadedIterator(iter(range(50)), max_queue_size=3)) == list(range(50))
+
+    def bad():
+        yield 1
+        raise KeyError("boom")
+    with pytest.raises(KeyError):
+        list(ThreadedIterator(bad()))
+    raw = synthetic_treebank(60, seed=3)
+    assert all(len(d["graph"]) == len(d["node_features"]) - 1 == len(d["targets"]) for d in raw)
+    assert all(0 <= e[0] < len(d["node_features"]) and 1 <= e[1] < 46 for d in raw for e in d["graph"])
+
+    class M(BtbBatching):
+        params = {"batch_size": 8, "output_size": 150, "task_ids": [0], "task_sample_ratios": {},
+                  "tie_fwd_bkwd": True, "graph_state_dropout_keep_prob": 0.9, "emb_dropout_keep_prob": 0.55,
+                  "out_layer_dropout_keep_prob": 0.85, "compact_adjacency": True}
+        num_edge_types, output_size_edges, pos_size, bucket_max_nodes = 46, 12, 46, 120
+    m = M()
+    data = m.process_raw_graphs(raw, False)
+    feeds = list(m.make_minibatch_iterator(data, False))
+    assert sum(f["num_graphs"] for f in feeds) == 60
+    for f in feeds:
+        assert f["adjacency_matrix"] is None and len(f["adjacency_edges"]) == f["num_graphs"]
+        assert f["word_inputs"].shape == (f["num_graphs"], f["num_vertices"], 6)

@@ -265,3 +265,32 @@ def test_checkpoint_restores_adam_step_past_float32_underflow(tmp_path):
     assert m2.optimizer.t == 4321
     for a, b in zip(m.optimizer.m, m2.optimizer.m):
         assert torch.equal(a, b)
+
+
+def test_run_epoch_end_to_end_reference_defaults():
+    """run_epoch (chem_tensorflow.py:528-667) with the reference's default
+    params (hidden_size 400, num_timesteps 4, batch_size 20, the 80/50/100/80
+    embedding widths, output_size 150 -- config 1's model; hidden 400 runs the
+    general path) on a synthetic treebank: the reference's return tuple, the
+    training loss falls over epochs, LAS/UAS are fractions, instances/sec > 0."""
+    _torch()
+    from ggnn_amd.batching import synthetic_treebank
+    from ggnn_amd.model import DenseGGNNChemModel
+    raw = synthetic_treebank(120, seed=1, max_nodes=60)
+    m = DenseGGNNChemModel(num_edge_types=46, output_size_edges=12, pos_size=46, vocab_size=39549,
+                           params={"compact_adjacency": True}, seed=0)
+    assert m.params["hidden_size"] == 400 and m.params["num_timesteps"] == 4 and m.params["batch_size"] == 20
+    train = m.process_raw_graphs(raw[:100], True)
+    valid = m.process_raw_graphs(raw[100:], False)
+    losses = []
+    for epoch in range(3):
+        r = m.run_epoch("epoch %d (train)" % epoch, train, True)
+        assert len(r) == 17
+        loss, acc, err, ips, steps, las, uas = r[:7]
+        assert np.isfinite(loss) and ips > 0 and steps >= 5 and 0 <= las <= uas <= 1
+        assert np.allclose(acc, [loss]) and np.allclose(err, acc / m.CHEMICAL_ACCURACIES[0])
+        losses.append(loss)
+    assert losses[-1] < losses[0]
+    v = m.run_epoch("valid", valid, False)
+    assert np.isfinite(v[0]) and 0 <= v[5] <= v[6] <= 1 and 0 <= v[16] <= 1
+    assert sum(x.shape[0] for x in v[8]) == 20      # all_computed_values cover the split
