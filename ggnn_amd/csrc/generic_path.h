@@ -85,9 +85,21 @@ template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
-  const dim3 grid((unsigned)((a.N + 63) / 64), (unsigned)((a.M + 63) / 64), (unsigned)std::min(a.Z, 65535));
+  // 128-row / 128-column block tiles (2 x 2 accumulators per wave) where the
+  // problem fills them; splits must stay tile-aligned
+  const int WM = (a.M >= 128 && a.Msplit % 128 == 0) ? 2 : 1;
+  const int WN = (WM == 2 && a.N >= 128 && a.Nsplit % 128 == 0) ? 2 : 1;
+  const dim3 grid((unsigned)((a.N + 64 * WN - 1) / (64 * WN)), (unsigned)((a.M + 64 * WM - 1) / (64 * WM)),
+                  (unsigned)std::min(a.Z, 65535));
   Prof p(kind, s);  // (kind < 0: no record, the caller's own Prof scope covers it)
-#define GGL(A16_, AKC_, BKC_) hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_>), grid, dim3(256), 0, s, a)
+#define GGW(A16_, AKC_, BKC_, WM_, WN_) \
+  hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_, WM_, WN_>), grid, dim3(256), 0, s, a)
+#define GGL(A16_, AKC_, BKC_)                             \
+  do {                                                    \
+    if (WM == 1) GGW(A16_, AKC_, BKC_, 1, 1);             \
+    else if (WN == 1) GGW(A16_, AKC_, BKC_, 2, 1);        \
+    else GGW(A16_, AKC_, BKC_, 2, 2);                     \
+  } while (0)
   if (A16 && AKC && !BKC) GGL(true, true, false);
   else if (A16 && !AKC && !BKC) GGL(true, false, false);
   else if (!A16 && AKC && !BKC) GGL(false, true, false);
@@ -95,6 +107,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   else if (!A16 && !AKC && !BKC) GGL(false, false, false);
   else return fail(GGNN_EINVAL, "k_gemm: operand layout combination not compiled");
 #undef GGL
+#undef GGW
   return GGNN_OK;
 }
 
@@ -321,8 +334,8 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
         hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * H * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
                            c.C, c.H, t, c.edrop);
       if (use_bias)
-        hipLaunchKernelGGL(k_gen_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C), dim3(256), 0, s, dM,
-                           P<const int>(adj, AL.cgl), c.b, c.C, c.vin, c.H, dbeta);
+        hipLaunchKernelGGL(k_gen_dbeta, dim3((unsigned)((H + 63) / 64), (unsigned)C, (unsigned)std::min(c.b, 64)),
+                           dim3(256), 0, s, dM, P<const int>(adj, AL.cgl), c.b, c.C, c.vin, c.H, dbeta);
     }
     // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
     {

@@ -972,6 +972,26 @@ int ggnn_backward(const ggnn_dims* d, const void* pack, const void* adj, void* w
   }
 }
 
+// ---- test / tuning hook: D[M][N] = A[M][K] B[K][N] (row-major fp32) through
+// k_gemm in the precision of d->flags (the general path's product kernel)
+int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const float* B, float* D,
+                  ggnn_stream_t stream) {
+  Cfg c;
+  if (int e = make_cfg(d, &c)) return e;
+  if (!A || !B || !D || M < 1 || N < 1 || K < 1) return fail(GGNN_EINVAL, "dbg_gemm: bad arguments");
+  GemmArgs a = gg_args();
+  a.A = A; a.sAm = K; a.sAk = 1;
+  a.B = B; a.sBk = N; a.sBn = 1;
+  a.D = D; a.sDm = N; a.sDn = 1;
+  a.M = M; a.N = N; a.K = K;
+  hipStream_t s = (hipStream_t)stream;
+  switch (c.prec) {
+    case PREC_SPLIT: return gg_launch<PREC_SPLIT>(a, false, true, false, K_PROP_FWD, s);
+    case PREC_F16: return gg_launch<PREC_F16>(a, false, true, false, K_PROP_FWD, s);
+    default: return gg_launch<PREC_BF16>(a, false, true, false, K_PROP_FWD, s);
+  }
+}
+
 // ---- embedding front-end and output heads (k_head.h)
 static int plain_dims(const ggnn_dims* d, const char* what) {
   if (!d) return fail(GGNN_EINVAL, std::string(what) + ": dims is NULL");

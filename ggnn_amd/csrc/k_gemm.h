@@ -177,15 +177,18 @@ DEV void gg_store(char* hi, char* lo, const float* x, int tid) {
   }
 }
 
-template <int PREC, bool A16, bool AKC, bool BKC>
+// WM x WN accumulators per wave: block tile (64 WM) x (64 WN), 4 waves in 2 x 2
+template <int PREC, bool A16, bool AKC, bool BKC, int WM, int WN>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   using namespace gg;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  constexpr int BMt = 64 * WM, BNt = 64 * WN;
+  constexpr int AT = BMt * PITCH, BT = BNt * PITCH, BUF = 2 * AT + 2 * BT;
   // [buf][A hi, A lo, B hi, B lo]
-  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * TILE];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int wm = w & 1, wn = w >> 1;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BNt, m0 = blockIdx.y * BMt;
   const int kc = (a.K + BK - 1) / BK;
 
   for (int z = blockIdx.z; z < a.Z; z += gridDim.z) {
@@ -198,8 +201,8 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
       q = a.tl ? a.tl[(long)z * a.ts + 1 + e] : zq + e;
     };
 
-    // ---- global -> registers: this thread's 8 A values and 8 B values of a stage
-    float ra[8], rb[8];
+    // ---- global -> registers: 8 values per 64-row share of each operand
+    float ra[8 * WM], rb[8 * WN];
     auto load = [&](int st) {
       int p, q;
       term(st / kc, p, q);
@@ -211,20 +214,35 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
       const int am0 = lowm ? m0 - a.Msplit : m0;
       const int aM = lowm ? a.M - a.Msplit : a.Msplit ? a.Msplit : a.M;
       const long abase = p * a.sAp + (second ? 0 : q * a.sAq);
-      if constexpr (A16)
-        gg_load<AKC, true, F16>(ra, Ab, abase, a.sAm, a.sAk, am0, aM, kk0, a.K, kg0, a.Ktot, 1.0f, tid);
-      else
-        gg_load<AKC, false, F16>(ra, Ab, abase, a.sAm, a.sAk, am0, aM, kk0, a.K, kg0, a.Ktot, a.scA, tid);
-      gg_load<BKC, false, F16>(rb, a.B, p * a.sBp + q * a.sBq, a.sBn, a.sBk, n0, a.N, kk0, a.K, kg0, a.Ktot, a.scB, tid);
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        if constexpr (A16)
+          gg_load<AKC, true, F16>(ra + 8 * i, Ab, abase, a.sAm, a.sAk, am0 + 64 * i, aM, kk0, a.K, kg0, a.Ktot, 1.0f,
+                                  tid);
+        else
+          gg_load<AKC, false, F16>(ra + 8 * i, Ab, abase, a.sAm, a.sAk, am0 + 64 * i, aM, kk0, a.K, kg0, a.Ktot, a.scA,
+                                   tid);
+      }
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        gg_load<BKC, false, F16>(rb + 8 * j, a.B, p * a.sBp + q * a.sBq, a.sBn, a.sBk, n0 + 64 * j, a.N, kk0, a.K, kg0,
+                                 a.Ktot, a.scB, tid);
     };
     // ---- registers -> LDS limb images ([row][k], k contiguous)
     auto store = [&](int buf) {
-      char* ah = smem + buf * 4 * TILE;
-      gg_store<AKC, F16, SPLIT && !A16>(ah, ah + TILE, ra, tid);
-      gg_store<BKC, F16, SPLIT>(ah + 2 * TILE, ah + 3 * TILE, rb, tid);
+      char* ah = smem + buf * BUF;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) gg_store<AKC, F16, SPLIT && !A16>(ah + 64 * i * PITCH, ah + AT + 64 * i * PITCH, ra + 8 * i, tid);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        gg_store<BKC, F16, SPLIT>(ah + 2 * AT + 64 * j * PITCH, ah + 2 * AT + BT + 64 * j * PITCH, rb + 8 * j, tid);
     };
 
-    f32x16 acc = splat(0.f);
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[i][j] = splat(0.f);
     if (nst > 0) {
       load(0);
       store(0);
@@ -233,22 +251,32 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     for (int st = 0; st < nst; ++st) {
       const bool more = st + 1 < nst;
       if (more) load(st + 1);
-      const char* ah = smem + (st & 1) * 4 * TILE;
-      const char* al = ah + TILE;
-      const char* bh = ah + 2 * TILE;
-      const char* bl = ah + 3 * TILE;
+      const char* ah = smem + (st & 1) * BUF;
+      const char* al = ah + AT;
+      const char* bh = ah + 2 * AT;
+      const char* bl = bh + BT;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
-        const int oa = (wm * 32 + l32) * PITCH + (2 * s + hh) * 16;
-        const int ob = (wn * 32 + l32) * PITCH + (2 * s + hh) * 16;
-        const frag fah = lds_frag(ah, oa), fbh = lds_frag(bh, ob);
-        const frag fbl = SPLIT ? lds_frag(bl, ob) : fbh;
-        if constexpr (A16) {
-          mma_xa<PREC>(acc, fah, fbh, fbl);
-        } else {
-          const frag fal = SPLIT ? lds_frag(al, oa) : fah;
-          mma<PREC>(acc, fah, fal, fbh, fbl);
+        frag fah[WM], fal[WM], fbh[WN], fbl[WN];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+          const int oa = (wm * 32 * WM + 32 * i + l32) * PITCH + (2 * s + hh) * 16;
+          fah[i] = lds_frag(ah, oa);
+          fal[i] = (SPLIT && !A16) ? lds_frag(al, oa) : fah[i];
         }
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const int ob = (wn * 32 * WN + 32 * j + l32) * PITCH + (2 * s + hh) * 16;
+          fbh[j] = lds_frag(bh, ob);
+          fbl[j] = SPLIT ? lds_frag(bl, ob) : fbh[j];
+        }
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            if constexpr (A16) mma_xa<PREC>(acc[i][j], fah[i], fbh[j], fbl[j]);
+            else mma<PREC>(acc[i][j], fah[i], fal[i], fbh[j], fbl[j]);
+          }
       }
       if (more) store((st + 1) & 1);
       __syncthreads();
@@ -257,24 +285,28 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
     // ---- epilogue
     const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
     const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
-    const int n = n0 + wn * 32 + l32;
-    if (n < a.N) {
-      const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 + acc_row(r, hh);
-        if (m >= a.M) continue;
-        float x = a.alpha * acc[r] + bn;
-        if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
-        else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-        const bool hi_n = a.Nsplit && n >= a.Nsplit;
-        const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
-        if (a.E) x *= a.E[doff];
-        float* d = (hi_n ? a.D2 : a.D) + doff;
-        if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-        else if (a.mode == GG_ADD) *d += x;
-        else *d = x;
-      }
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + wn * 32 * WN + 32 * j + l32;
+      if (n >= a.N) continue;
+      const float bn = bias ? bias[n] : 0.f;
+      const bool hi_n = a.Nsplit && n >= a.Nsplit;
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
+          if (m >= a.M) continue;
+          float x = a.alpha * acc[i][j][r] + bn;
+          if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
+          else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+          const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+          if (a.E) x *= a.E[doff];
+          float* d = (hi_n ? a.D2 : a.D) + doff;
+          if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+          else if (a.mode == GG_ADD) *d += x;
+          else *d = x;
+        }
     }
     __syncthreads();  // the next z's prologue rewrites buffer 0
   }

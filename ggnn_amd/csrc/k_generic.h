@@ -197,16 +197,25 @@ __global__ void k_gen_colsum(const float* __restrict__ X, long rows, int ncol, l
   for (long r = r0; r < r1; ++r) s += X[r * ld + n];
   if (r1 > r0) atomicAdd(out + n, s);
 }
-// dbeta[c][n] += sum over the graphs g of channel c and nodes j of dM[g][c][j][n]
-__global__ void k_gen_dbeta(const float* __restrict__ dM, const int* __restrict__ cgl, int b, int C, int v, int H,
-                            float* __restrict__ dbeta) {
-  const int c = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= H) return;
+// dbeta[c][n] += sum over the graphs g of channel c and nodes j of dM[g][c][j][n]:
+// grid (column blocks of 64, C, graph slices); 4 row groups per block summed in
+// LDS, one atomic per column per block
+__global__ void __launch_bounds__(256) k_gen_dbeta(const float* __restrict__ dM, const int* __restrict__ cgl, int b,
+                                                   int C, int v, int H, float* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.y, n = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
   const int* L = cgl + (long)c * (b + 1);
+  const int ng = L[0];
+  const int per = (ng + gridDim.z - 1) / gridDim.z;
+  const int e0 = blockIdx.z * per, e1 = min(ng, e0 + per);
   float s = 0.f;
-  for (int e = 0; e < L[0]; ++e) {
-    const float* p = dM + ((long)L[1 + e] * C + c) * v * H + n;
-    for (int j = 0; j < v; ++j) s += p[(long)j * H];
-  }
-  dbeta[(long)c * H + n] += s;
+  if (n < H)
+    for (int e = e0; e < e1; ++e) {
+      const float* p = dM + ((long)L[1 + e] * C + c) * v * H + n;
+      for (int j = rg; j < v; j += 4) s += p[(long)j * H];
+    }
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && n < H && e1 > e0)
+    atomicAdd(dbeta + (long)c * H + n, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
 }

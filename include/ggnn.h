@@ -130,6 +130,12 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack,
                       const float* candidate_kernel, const float* candidate_bias,
                       ggnn_stream_t stream);
 
+/* Test / tuning hook: D[M][N] = A[M][K] B[K][N], row-major fp32 device
+ * buffers, through the general path's MFMA product kernel (k_gemm) in the
+ * precision policy of d->flags (other fields of d: any valid dims). */
+int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const float* B, float* D,
+                  ggnn_stream_t stream);
+
 /* Stage one batch's adjacency [b][C][v][v] fp32 (0/1) into `adj` (sized by
  * ggnn_adjacency_bytes): 16-bit (exact for 0/1; bf16, or f16 under GGNN_FP16 /
  * GGNN_FP32_PARITY), its transpose, per-node in-degrees and the per-graph list

@@ -141,3 +141,31 @@ def test_generic_bf16_statistical():
     assert _nrms(got["hT"], ref) <= 2e-2
     for k in GRADS:
         assert _nrms(got[k].reshape(gref[k].shape), gref[k]) <= 5e-2, k
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 150, 61), (130, 129, 257), (256, 512, 96), (512, 64, 1000)])
+@pytest.mark.parametrize("precision", ["fp32", "fp16", "bf16"])
+def test_k_gemm_against_numpy(M, N, K, precision):
+    """The general path's product kernel on its own (ggnn_dbg_gemm): ragged
+    shapes across the 64/128-row tile variants; fp32-parity mode within 1e-6 of
+    float64 relative to the accumulated magnitude, 16-bit modes within their
+    operand rounding."""
+    torch = _torch()
+    import ctypes
+    from ggnn_amd import _lib
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    a, b = torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev)
+    d = torch.full((M, N), float("nan"), device=dev)
+    dims = _lib.dims(1, 1, 64, 1, 1, True, precision)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.load().ggnn_dbg_gemm(ctypes.byref(dims), M, N, K, ctypes.c_void_p(a.data_ptr()),
+                                         ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(d.data_ptr()), s),
+               "ggnn_dbg_gemm")
+    got = d.cpu().numpy()
+    ref = A.astype(np.float64) @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+    err = float(np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)))
+    assert err <= {"fp32": 1e-6, "fp16": 2e-3, "bf16": 1e-2}[precision], err
