@@ -105,7 +105,8 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   if (!d) return fail(GGNN_EINVAL, "dims is NULL");
   if (d->b < 1 || d->v < 1 || d->C < 1 || d->T < 1) return fail(GGNN_EINVAL, "dims: b, v, C, T must be >= 1");
   if (d->h < 1 || d->h > 4096) return fail(GGNN_EUNSUP, "hidden size must lie in 1..4096 (got " + std::to_string(d->h) + ")");
-  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS | GGNN_GENERIC))
+  if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS | GGNN_GENERIC |
+                   GGNN_UNFUSED_FWD))
     return fail(GGNN_EINVAL, "unknown flag bits");
   // the specialised kernels: hidden 128 / 256, v <= 128; everything else runs
   // the general path (generic_path.h)
@@ -216,7 +217,7 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.hb[0] = o; o += nh2;
     L.hb[1] = o; o += nh2;
   }
-  L.Xa = o; o += L.nha;
+  L.Xa = o; o += L.nh4;  // fp32 X scratch of the fused forward (k_fused.h) in every mode; 16-bit X otherwise
   if (!training) {
     L.hf[0] = o; o += L.nh4;
     L.hf[1] = o; o += L.nh4;
@@ -378,19 +379,20 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   // place (training copies h0: the backward needs it after the caller's buffer
   // may have changed)
   const bool dense = c.vin == c.V;
+  // the whole T-step forward of each graph in one workgroup (k_fused.h)
+  const bool fused = c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT && !(c.flags & GGNN_UNFUSED_FWD);
   float* hf0 = tr ? P<float>(ws, L.hfT) : P<float>(ws, L.hf[0]);
   if (tr) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL((k_stage_h0<Prec<PREC>::f16>), dim3((N + 63) / 64, H / 64), dim3(256), 0, s, h0, c.vin, c.V,
                        hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), P<u16>(ws, L.hT), N, c.H);
-  } else if (!dense || !SPLIT) {
+  } else if (!dense || (!SPLIT && !fused)) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H,
                        dense ? (float*)nullptr : hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N,
                        (int)Prec<PREC>::f16, kNoDrop, 0, (const uint32_t*)nullptr);
   }
-  if (SPLIT && c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT) {
-    // the whole T-step forward of each graph in one workgroup (k_fused.h)
+  if (fused) {
     FusedFwdArgs fa;
     memset(&fa, 0, sizeof(fa));
     fa.Ab = P<u16>(adj, AL.Ab);
@@ -428,7 +430,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     fa.sd = c.sdrop;
     {
       Prof p(K_FWD_FUSED, s);
-      hipLaunchKernelGGL(k_fwd_fused, dim3(c.b), dim3(512), 0, s, fa);
+      hipLaunchKernelGGL(k_fwd_fused<PREC>, dim3(c.b), dim3(512), 0, s, fa);
     }
   } else
   for (int t = 0; t < c.T; ++t) {

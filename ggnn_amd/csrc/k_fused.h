@@ -48,8 +48,20 @@ struct FusedFwdArgs {
   Drop sd;
 };
 
+// PREC: PREC_SPLIT (fp32-parity: f16 hi/lo limb images, 3 products) or a
+// single-limb 16-bit mode (bf16 / f16: one image, one product; the same
+// rounding points as the unfused k_prop_fwd + k_gru_fwd path: h, M, X, r*h)
+template <int PREC>
 __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
   using namespace gru2;
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  // chunk -> ring slot / image limbs
+  auto cput = [&](char* hi, char* lo, int off, const Chunk& v) {
+    const float x[8] = {__uint_as_float(v.a.x), __uint_as_float(v.a.y), __uint_as_float(v.a.z), __uint_as_float(v.a.w),
+                        __uint_as_float(v.b.x), __uint_as_float(v.b.y), __uint_as_float(v.b.z), __uint_as_float(v.b.w)};
+    st16(hi + off, pk8<F16>(x));
+    if constexpr (SPLIT) st16(lo + off, pk8_lo<true>(x));
+  };
   constexpr int V = 128, VT = 4, ACH = V / 8;
   typedef Swz<ACH> SA;
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 4 * SLOT];
@@ -80,8 +92,8 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       const int row = q & (R - 1), ch = q >> 7;  // consecutive lanes: consecutive rows of one chunk
       const float4 x0 = *(const float4*)(h0 + row * H + ch * 8), x1 = *(const float4*)(h0 + row * H + ch * 8 + 4);
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      st16(img_hi + koff(row, ch), pk8<true>(x));
-      st16(img_lo + koff(row, ch), pk8_lo<true>(x));
+      st16(img_hi + koff(row, ch), pk8<F16>(x));
+      if constexpr (SPLIT) st16(img_lo + koff(row, ch), pk8_lo<true>(x));
     }
   }
   if (nc > 0) glds_tile<ACH, V, NT>(abuf, ag + (long)chan(0) * V * V, (int)threadIdx.x);
@@ -115,8 +127,10 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
     };
     const int vr = ((ns * KSG) * 64 + lane) * 16, vu = (((NS + ns) * KSG) * 64 + lane) * 16;
     const int vw = ((ns * KS) * 64 + lane) * 16;  // strip ns of a [H][H] pack
-    auto ldg = [&](int k) { return F4{wld(wgh, vr, k), wld(wgl, vr, k), wld(wgh, vu, k), wld(wgl, vu, k)}; };
-    auto ldc = [&](int k) { return F2{wld(wch, vr, k), wld(wcl, vr, k)}; };
+    auto ldg = [&](int k) {
+      return F4{wld(wgh, vr, k), SPLIT ? wld(wgl, vr, k) : frag{}, wld(wgh, vu, k), SPLIT ? wld(wgl, vu, k) : frag{}};
+    };
+    auto ldc = [&](int k) { return F2{wld(wch, vr, k), SPLIT ? wld(wcl, vr, k) : frag{}}; };
     const long wt = (long)t * a.wstep;
     const rsrc_t wfh = mkrsrc(a.Wp + wt, C * H * H * 2), wfl = mkrsrc(a.Wp + wt + a.wlo, C * H * H * 2);
     // ===================== messages: X = sum_c A_c (h W_c + beta_c) =====================
@@ -130,25 +144,28 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) accm[rt] = splat(bb);
       const int cw = c * H * H * 2;
-      auto ldw = [&](int ks) { return F2{bld16(wfh, vw, cw + ks * 1024), bld16(wfl, vw, cw + ks * 1024)}; };
+      auto ldw = [&](int ks) {
+        return F2{bld16(wfh, vw, cw + ks * 1024), SPLIT ? bld16(wfl, vw, cw + ks * 1024) : frag{}};
+      };
       b_pipeline<KS, 2>(ldw, [&](int ks, const F2& w) {
 #pragma unroll
         for (int rt = 0; rt < VT; ++rt) {
           const int off = koff(rt * 32 + l32, 2 * ks + hh);
-          mma<PREC_SPLIT>(accm[rt], lds_frag(img_hi, off), lds_frag(img_lo, off), w.a, w.b);
+          const frag ah = lds_frag(img_hi, off);
+          mma<PREC>(accm[rt], ah, SPLIT ? lds_frag(img_lo, off) : ah, w.a, w.b);
         }
       });
       __syncthreads();  // S1: A_c visible
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
-        const frag mh0 = acc_hi<true>(accm[rt], 0), mh1 = acc_hi<true>(accm[rt], 1);
-        const frag ml0 = acc_lo<true>(accm[rt], 0), ml1 = acc_lo<true>(accm[rt], 1);
+        const frag mh0 = acc_hi<F16>(accm[rt], 0), mh1 = acc_hi<F16>(accm[rt], 1);
+        const frag ml0 = SPLIT ? acc_lo<true>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<true>(accm[rt], 1) : mh1;
 #pragma unroll
         for (int it = 0; it < VT; ++it) {
           const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
           const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
-          mma_xa<PREC_SPLIT>(accx[it], a0, mh0, ml0);
-          mma_xa<PREC_SPLIT>(accx[it], a1, mh1, ml1);
+          mma_xa<PREC>(accx[it], a0, mh0, ml0);
+          mma_xa<PREC>(accx[it], a1, mh1, ml1);
         }
       }
       __syncthreads();  // S2: A_c reads done
@@ -166,7 +183,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       for (int it = 0; it < VT; ++it)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          st_col4w<PREC_SPLIT>(xt + wg_off(n, row0 + it * 32 + 4 * hh, H) + 8 * q, accx[it][4 * q],
+          st_col4w<PREC>(xt + wg_off(n, row0 + it * 32 + 4 * hh, H) + 8 * q, accx[it][4 * q],
                                accx[it][4 * q + 1], accx[it][4 * q + 2], accx[it][4 * q + 3]);
     }
     __syncthreads();  // X visible to every wave
@@ -189,9 +206,9 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const int off = koff(rt * 32 + l32, 2 * (ks + s) + hh);
-          const frag ah = lds_frag(img_hi, off), al = lds_frag(img_lo, off);
-          mma<PREC_SPLIT>(ar[rt], ah, al, w.a, w.b);
-          mma<PREC_SPLIT>(au[rt], ah, al, w.c, w.d);
+          const frag ah = lds_frag(img_hi, off), al = SPLIT ? lds_frag(img_lo, off) : ah;
+          mma<PREC>(ar[rt], ah, al, w.a, w.b);
+          mma<PREC>(au[rt], ah, al, w.c, w.d);
         }
         const int nk = ks + s + 2;  // runs on into the x rows (k-steps 0, 1)
         const F4 nw = ldg(nk < KS ? KS + nk : nk - KS);
@@ -200,13 +217,13 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    chunk_put(slot_hi(0), slot_lo(0), cso, st0);
+    cput(slot_hi(0), slot_lo(0), cso, st0);
     st0 = xld(2);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NCHK; ++c) {
       if (c + 1 < NCHK) {
-        chunk_put(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
+        cput(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
         if (c + 3 < NCHK) {
           if (c & 1) st0 = xld(c + 3);
           else st1 = xld(c + 3);
@@ -219,9 +236,9 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const int off = koff(rt * 32 + l32, 2 * s + hh);
-          const frag ah = lds_frag(slot_hi(c & 1), off), al = lds_frag(slot_lo(c & 1), off);
-          mma<PREC_SPLIT>(ar[rt], ah, al, w.a, w.b);
-          mma<PREC_SPLIT>(au[rt], ah, al, w.c, w.d);
+          const frag ah = lds_frag(slot_hi(c & 1), off), al = SPLIT ? lds_frag(slot_lo(c & 1), off) : ah;
+          mma<PREC>(ar[rt], ah, al, w.a, w.b);
+          mma<PREC>(au[rt], ah, al, w.c, w.d);
         }
         const F4 nw = ldg(min(ks + 2, KS - 1));
         if (s) w1 = nw;
@@ -237,6 +254,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 
     // ========== r*h in place over the h image; r and (r*h)^T to HBM ==========
     {
+      const rsrc_t rh32 = mkrsrc(a.hf[t] + row0 * H, R * H * 4);
       u16* rht = a.rhT ? a.rhT + t * a.sw : nullptr;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
@@ -247,10 +265,16 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
           const float rr = sigm(ar[rt][r]);
           rv[r] = rr;
           const int eo = koff(rt * 32 + acc_row(r, hh), n >> 3) + (n & 7) * 2;
-          const float hx = from_limb<true>(*(const u16*)(img_hi + eo)) + from_limb<true>(*(const u16*)(img_lo + eo));
+          // h: the image's hi + lo limbs (split), or the fp32 state in the
+          // 16-bit modes (the unfused path forms r*h from the fp32 h too)
+          float hx;
+          if constexpr (SPLIT)
+            hx = from_limb<true>(*(const u16*)(img_hi + eo)) + from_limb<true>(*(const u16*)(img_lo + eo));
+          else
+            hx = bld(rh32, vo, (rt * 32 + acc_row0(r)) * H * 4);
           rh[r] = rr * hx;
-          *(u16*)(img_hi + eo) = to_limb<true>(rh[r]);
-          *(u16*)(img_lo + eo) = to_limb<true>(lo_part<true>(rh[r]));
+          *(u16*)(img_hi + eo) = to_limb<F16>(rh[r]);
+          if constexpr (SPLIT) *(u16*)(img_lo + eo) = to_limb<true>(lo_part<true>(rh[r]));
         }
         if (a.r) {  // row-quad-major save (ggnn_common.h: qm_vo)
 #pragma unroll
@@ -261,12 +285,12 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         if (rht) {
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            st_col4w<PREC_SPLIT>(rht + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, rh[4 * q], rh[4 * q + 1],
+            st_col4w<PREC>(rht + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, rh[4 * q], rh[4 * q + 1],
                                  rh[4 * q + 2], rh[4 * q + 3]);
         }
       }
     }
-    chunk_put(slot_hi(0), slot_lo(0), cso, st0);
+    cput(slot_hi(0), slot_lo(0), cso, st0);
     st0 = xld(2);
     __syncthreads();
 
@@ -288,7 +312,8 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
             const int off = koff(rt * 32 + l32, 2 * (ks + s) + hh);
-            mma<PREC_SPLIT>(ac[rt], lds_frag(img_hi, off), lds_frag(img_lo, off), w.a, w.b);
+            const frag ah = lds_frag(img_hi, off);
+            mma<PREC>(ac[rt], ah, SPLIT ? lds_frag(img_lo, off) : ah, w.a, w.b);
           }
           const int nk = ks + s + 2;
           const F2 nw = ldc(nk < KS ? KS + nk : nk - KS);
@@ -303,7 +328,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
     for (int c = 0; c < NCHK; ++c) {
       if (c + 1 < NCHK) {
-        chunk_put(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
+        cput(slot_hi((c + 1) & 1), slot_lo((c + 1) & 1), cso, (c & 1) ? st0 : st1);
         if (c + 3 < NCHK) {
           if (c & 1) st0 = xld(c + 3);
           else st1 = xld(c + 3);
@@ -316,7 +341,8 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const int off = koff(rt * 32 + l32, 2 * s + hh);
-          mma<PREC_SPLIT>(ac[rt], lds_frag(slot_hi(c & 1), off), lds_frag(slot_lo(c & 1), off), w.a, w.b);
+          const frag ah = lds_frag(slot_hi(c & 1), off);
+          mma<PREC>(ac[rt], ah, SPLIT ? lds_frag(slot_lo(c & 1), off) : ah, w.a, w.b);
         }
         const F2 nw = ldc(min(ks + 2, KS - 1));
         if (s) w1 = F4{nw.a, nw.b, nw.a, nw.b};
@@ -377,15 +403,17 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int eo = koff(rt * 32 + 8 * q + 4 * hh + (l32 & 3), n >> 3) + (n & 4) * 2;
-          const v2u32 wh = quad_transpose4(pk<true>(hn[4 * q], hn[4 * q + 1]), pk<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
-          const v2u32 wl = quad_transpose4(pk_lo<true>(hn[4 * q], hn[4 * q + 1]), pk_lo<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
+          const v2u32 wh = quad_transpose4(pk<F16>(hn[4 * q], hn[4 * q + 1]), pk<F16>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
           *(uint2*)(img_hi + eo) = make_uint2(wh.x, wh.y);
-          *(uint2*)(img_lo + eo) = make_uint2(wl.x, wl.y);
+          if constexpr (SPLIT) {
+            const v2u32 wl = quad_transpose4(pk_lo<true>(hn[4 * q], hn[4 * q + 1]), pk_lo<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
+            *(uint2*)(img_lo + eo) = make_uint2(wl.x, wl.y);
+          }
         }
         if (hto) {
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            st_col4w<PREC_SPLIT>(hto + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, hn[4 * q], hn[4 * q + 1],
+            st_col4w<PREC>(hto + wg_off(n, row0 + rt * 32 + 4 * hh, H) + 8 * q, hn[4 * q], hn[4 * q + 1],
                                  hn[4 * q + 2], hn[4 * q + 3]);
         }
       }

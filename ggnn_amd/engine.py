@@ -58,7 +58,8 @@ class PropagationEngine:
     and its backward for batches of shape [b, C, v, v] / [b, v, h]."""
 
     def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None,
-                 precision: str = "fp32", skip_empty_channels: bool = True, force_generic: bool = False):
+                 precision: str = "fp32", skip_empty_channels: bool = True, force_generic: bool = False,
+                 unfused_forward: bool = False):
         """precision: "fp32" (GGNN_FP32_PARITY, the default: every non-exact MFMA
         operand of the propagation as an f16 hi/lo limb pair, fp32 accumulation,
         matches the reference's fp32 math to <= 1e-3), "fp16" or "bf16" (single
@@ -67,7 +68,9 @@ class PropagationEngine:
         non-empty adjacency channels (bit-identical; False = GGNN_DENSE_CHANNELS).
         force_generic: run the general path (k_gemm products) even where the
         specialised kernels apply (hidden 128 / 256, v <= 128); other shapes
-        always take it (GGNN_GENERIC)."""
+        always take it (GGNN_GENERIC).  unfused_forward: per-timestep
+        k_prop_fwd + k_gru_fwd launches instead of the one-launch fused forward
+        at hidden 256, v <= 128 (GGNN_UNFUSED_FWD; A/B and tests)."""
         self.h = int(hidden)
         self.C = int(channels)
         self.use_edge_bias = bool(use_edge_bias)
@@ -76,6 +79,7 @@ class PropagationEngine:
         self.precision = precision
         self.skip_empty_channels = bool(skip_empty_channels)
         self.force_generic = bool(force_generic)
+        self.unfused_forward = bool(unfused_forward)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._lib = _lib.load()
         self._adj = None            # staged adjacency buffer
@@ -88,7 +92,7 @@ class PropagationEngine:
     def dims(self, b: int, v: int, T: int, edge_keep: float = 1.0, state_keep: float = 1.0,
              seed: int = 0) -> _lib.GGNNDims:
         d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision, edge_keep, state_keep, seed,
-                      self.skip_empty_channels, self.force_generic)
+                      self.skip_empty_channels, self.force_generic, self.unfused_forward)
         _lib.check_dims(d)
         return d
 

@@ -86,6 +86,9 @@ enum {
  * 198-node buckets, chem_tensorflow_dense.py:584-585); GGNN_GENERIC forces it
  * for every shape (parity tests, A/B). */
 #define GGNN_GENERIC 16
+/* Run the forward of hidden 256, v <= 128 batches as per-timestep k_prop_fwd +
+ * k_gru_fwd launches instead of the one-launch fused forward (A/B and tests). */
+#define GGNN_UNFUSED_FWD 32
 
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */

@@ -56,12 +56,12 @@ def _f64(w):
     return {k: x.astype(np.float64) for k, x in w.items()}
 
 
-def _run(A, h0, w, T, precision, use_bias=True, dhT=None, skip=True, generic=False):
+def _run(A, h0, w, T, precision, use_bias=True, dhT=None, skip=True, generic=False, unfused=False):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, C, v, _ = A.shape
     eng = PropagationEngine(h0.shape[-1], C, use_edge_bias=use_bias, precision=precision, skip_empty_channels=skip,
-                            force_generic=generic)
+                            force_generic=generic, unfused_forward=unfused)
     dev = eng.device
     pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()})
     eng.set_adjacency(torch.from_numpy(np.ascontiguousarray(A)).to(dev))
@@ -680,3 +680,34 @@ def test_bf16_within_north_star_on_dependency_trees(v, parity_bias):
     assert errs["hT_nrms"] <= BF16_RMS_TOL and errs["hT_max"] <= BF16_RMS_TOL
     for k in GRADS:
         assert errs[k] <= BF16_RMS_TOL, (k, errs[k])
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_fused_forward_16bit_matches_unfused(precision):
+    """k_fwd_fused in the single-limb modes (one launch for all T timesteps,
+    h in LDS) against the per-timestep k_prop_fwd + k_gru_fwd launches: the
+    same rounding points (h, M, X, r*h), so they differ only through fp32
+    accumulation order (and the rare 1-ulp flips of a 16-bit operand it
+    causes).  One timestep on the dense synthetic data; T = 5 with the
+    backward on dependency-tree graphs (the dense synthetic data amplifies a
+    flip through the saturated GRU, see test_bf16_within_north_star_...)."""
+    b, v, h, C, T = 3, 128, 256, 8, 1
+    A, h0, w = _case(b, v, h, C, seed=41)
+    fu = _run(A, h0, w, T, precision)["hT"]
+    un = _run(A, h0, w, T, precision, unfused=True)["hT"]
+    d = np.abs(fu - un)
+    assert np.median(d) <= 1e-6 and d.mean() <= 1e-5 and d.max() <= 1e-2, (np.median(d), d.mean(), d.max())
+    E, T = 46, 5
+    A = _tree_adjacency(b, v, E, seed=5, zipf=True, first_empty=False)
+    rng = np.random.default_rng(9)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=2)
+    dhT = rng.standard_normal((b, v, h)).astype(np.float32)
+    fu = _run(A, h0, w, T, precision, dhT=dhT)
+    un = _run(A, h0, w, T, precision, dhT=dhT, unfused=True)
+    # (bf16's own error vs float64 here is ~4e-3: a half-ulp-scale difference)
+    assert _nrms(fu["hT"], un["hT"]) <= 5e-3, _nrms(fu["hT"], un["hT"])
+    for k in GRADS:
+        assert _nrms(fu[k], un[k]) <= 1e-2, (k, _nrms(fu[k], un[k]))
+    inf = _run(A, h0, w, T, precision)   # inference workspace
+    assert _nrms(inf["hT"], fu["hT"]) <= 5e-3
