@@ -85,21 +85,14 @@ template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
-  // 128-row / 128-column block tiles (2 x 2 accumulators per wave) where the
-  // problem fills them; splits must stay tile-aligned
-  const int WM = (a.M >= 128 && a.Msplit % 128 == 0) ? 2 : 1;
-  const int WN = (WM == 2 && a.N >= 128 && a.Nsplit % 128 == 0) ? 2 : 1;
-  const dim3 grid((unsigned)((a.N + 64 * WN - 1) / (64 * WN)), (unsigned)((a.M + 64 * WM - 1) / (64 * WM)),
-                  (unsigned)std::min(a.Z, 65535));
+  // 64 x 64 block tiles: measured faster than the 128 x 64 / 128 x 128
+  // variants of k_gemm on every shape tried (tools/gemm_probe.py: 4096^3, the
+  // heads' 32768 x {150, 512} x {512, 150, 256}, a per-graph 128 x 256 x 256):
+  // the bigger tiles lose more to occupancy than they save in operand
+  // conversion per MFMA
+  const dim3 grid((unsigned)((a.N + 63) / 64), (unsigned)((a.M + 63) / 64), (unsigned)std::min(a.Z, 65535));
   Prof p(kind, s);  // (kind < 0: no record, the caller's own Prof scope covers it)
-#define GGW(A16_, AKC_, BKC_, WM_, WN_) \
-  hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_, WM_, WN_>), grid, dim3(256), 0, s, a)
-#define GGL(A16_, AKC_, BKC_)                             \
-  do {                                                    \
-    if (WM == 1) GGW(A16_, AKC_, BKC_, 1, 1);             \
-    else if (WN == 1) GGW(A16_, AKC_, BKC_, 2, 1);        \
-    else GGW(A16_, AKC_, BKC_, 2, 2);                     \
-  } while (0)
+#define GGL(A16_, AKC_, BKC_) hipLaunchKernelGGL((k_gemm<PREC, A16_, AKC_, BKC_, 1, 1>), grid, dim3(256), 0, s, a)
   if (A16 && AKC && !BKC) GGL(true, true, false);
   else if (A16 && !AKC && !BKC) GGL(true, false, false);
   else if (!A16 && AKC && !BKC) GGL(false, true, false);
@@ -107,7 +100,6 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   else if (!A16 && !AKC && !BKC) GGL(false, false, false);
   else return fail(GGNN_EINVAL, "k_gemm: operand layout combination not compiled");
 #undef GGL
-#undef GGW
   return GGNN_OK;
 }
 
