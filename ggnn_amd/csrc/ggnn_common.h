@@ -154,7 +154,7 @@ DEV frag lds_frag(const char* img, int off) { return ld16(img + off); }
 // 16*lane), so the swizzle goes on the SOURCE address: LDS slot (row, pc)
 // receives logical chunk pc ^ (row & M), the same involution Swz::off reads
 // with.  No VGPR staging; completion is on vmcnt (a __syncthreads drains it).
-template <int NCH, int R, int NT>
+template <int NCH, int R, int NT, int AUX = 0>
 DEV void glds_tile(char* lds, const u16* src, int tid) {
   typedef Swz<NCH> S;
   constexpr int TOT = R * NCH;
@@ -165,7 +165,7 @@ DEV void glds_tile(char* lds, const u16* src, int tid) {
     if (qb < TOT) {
       const int q = qb + lane, row = q / NCH, pc = q % NCH;
       __builtin_amdgcn_global_load_lds((const void*)(src + (row * NCH + (pc ^ (row & S::M))) * 8),
-                                       (__attribute__((address_space(3))) void*)(lds + qb * 16), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(lds + qb * 16), 16, 0, AUX);
     }
   }
 }

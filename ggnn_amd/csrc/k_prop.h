@@ -7,6 +7,12 @@
 #pragma once
 #include "ggnn_common.h"
 
+// cache policy of the adjacency LDS-DMA: nontemporal (each tile is read once
+// per launch; measured -1.5 % on k_prop_bwd)
+#ifndef GGNN_PROP_A_AUX
+#define GGNN_PROP_A_AUX kNT
+#endif
+
 // ===========================================================================
 // k_prop_fwd: per channel c
 //   MT : M_c = h W_c + beta_c                 (K = H; h from LDS, W_c from the
@@ -53,9 +59,9 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 
   stage_rows_k<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
-  if (nc > 0) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)chan(0) * V * V, tid);
+  if (nc > 0) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(0), ag + (long)chan(0) * V * V, tid);
   __syncthreads();
-  if (NAB == 2 && nc > 1) glds_tile<ACH, V, NT>(abuf_of(1), ag + (long)chan(1) * V * V, tid);
+  if (NAB == 2 && nc > 1) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(1), ag + (long)chan(1) * V * V, tid);
 
   f32x16 accx[VT];
 #pragma unroll
@@ -86,7 +92,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
     __syncthreads();  // S1: A_c visible (two tiles: and every wave is past AGG(c-1))
-    if (NAB == 2 && ci >= 1 && ci + 1 < nc) glds_tile<ACH, V, NT>(abuf_of(ci + 1), ag + (long)chan(ci + 1) * V * V, tid);
+    if (NAB == 2 && ci >= 1 && ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(ci + 1), ag + (long)chan(ci + 1) * V * V, tid);
     const char* abuf = abuf_of(ci);
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
@@ -104,7 +110,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (NAB == 1) {
       __syncthreads();  // S2: A_c reads done
       // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
-      if (ci + 1 < nc) glds_tile<ACH, V, NT>(abuf_of(0), ag + (long)chan(ci + 1) * V * V, tid);
+      if (ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(0), ag + (long)chan(ci + 1) * V * V, tid);
     }
   }
 
@@ -192,7 +198,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   const int nc = cl[0];
   auto chan = [&](int i) { return cl[1 + i]; };
   const u16* ag = AbT + (long)g * C * V * V;
-  if (nc > 0) glds_tile<ACH, V, NT>(abuf, ag + (long)chan(0) * V * V, tid);
+  if (nc > 0) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf, ag + (long)chan(0) * V * V, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
   const int vo = (4 * hh * H + n) * 4;
   f32x16 adh[VT];
@@ -245,7 +251,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
     // A_{c+1} lands in LDS by DMA while phase b runs (drained by S2)
-    if (ci + 1 < nc) glds_tile<ACH, V, NT>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
+    if (ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
     auto ldb = [&](int ks) {
