@@ -367,6 +367,18 @@ DEV void gst4(void* base, int voff, int soff, float4 v) {
 DEV float4 bld4(rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
+// the same with a cache-policy operand (kNT: nontemporal)
+template <int AUX> DEV float bld_p(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
+}
+template <int AUX> DEV float4 bld4_p(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+}
+// 16-byte nontemporal global store (saddr form as gst4)
+DEV void gst4_nt(void* base, int voff, int soff, float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, (f4v*)((char*)base + soff + (unsigned long)(unsigned)voff));
+}
 
 // ---- store 4 consecutive rows (acc regs 4q..4q+3) of one column into a
 // transposed [col][row] activation array (rows contiguous)

@@ -25,6 +25,9 @@
 #define FUSED_MAXT 16
 // cache policy of the adjacency LDS-DMA: nontemporal (the tiles are read once
 // per timestep; measured -1.5 % on the kernel, less L2 pollution for the X scratch)
+#ifndef GGNN_FUSED_SAVE_NT
+#define GGNN_FUSED_SAVE_NT 0  // nontemporal r / u / c saves: measured no gain, off
+#endif
 #ifndef GGNN_FUSED_A_AUX
 #define GGNN_FUSED_A_AUX kNT
 #endif
@@ -284,7 +287,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         if (a.r) {  // row-quad-major save (ggnn_common.h: qm_vo)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            gst4(a.r + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.r + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]));
         }
         if (rht) {
@@ -398,9 +401,9 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         if (sav) {  // row-quad-major saves
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            gst4(a.u + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.u + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(uv[4 * q], uv[4 * q + 1], uv[4 * q + 2], uv[4 * q + 3]));
-            gst4(a.c + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.c + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(cv[4 * q], cv[4 * q + 1], cv[4 * q + 2], cv[4 * q + 3]));
           }
         }

@@ -9,6 +9,9 @@
 
 // cache policy of the adjacency LDS-DMA: nontemporal (each tile is read once
 // per launch; measured -1.5 % on k_prop_bwd)
+#ifndef GGNN_PB_AUX
+#define GGNN_PB_AUX 0  // cache policy of k_prop_bwd's dh_in loads
+#endif
 #ifndef GGNN_PROP_A_AUX
 #define GGNN_PROP_A_AUX kNT
 #endif
@@ -205,7 +208,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) adh[jt][r] = bld(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
+    for (int r = 0; r < 16; ++r) adh[jt][r] = bld_p<GGNN_PB_AUX>(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
   __syncthreads();
 
   for (int ci = 0; ci < nc; ++ci) {
