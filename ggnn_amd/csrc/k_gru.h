@@ -17,6 +17,9 @@
 #ifndef GGNN_GB_AUX
 #define GGNN_GB_AUX kNT
 #endif
+#ifndef GGNN_GB_H_AUX
+#define GGNN_GB_H_AUX 0  // the state h (read in both phases): experiment
+#endif
 
 // weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
 // full unrolling, which spills at H = 256)
@@ -266,7 +269,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld_p<GGNN_GB_AUX>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld(ph, vo, so);
+        const float d = bld_p<GGNN_GB_AUX>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld_p<GGNN_GB_H_AUX>(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
         du[rt][4 * q + i] = d * u;
@@ -320,7 +323,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         const int r = 4 * q + i;
         const int ro = rt * 32 + acc_row0(r);
         const int so = ro * H * 4;
-        const float h = bld(ph, vo, so), rr = rq[i];
+        const float h = bld_p<GGNN_GB_H_AUX>(ph, vo, so), rr = rq[i];
         const float drh = a2[rt][r];
         a2[rt][r] = du[rt][r] + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);

@@ -10,7 +10,10 @@
 // cache policy of the adjacency LDS-DMA: nontemporal (each tile is read once
 // per launch; measured -1.5 % on k_prop_bwd)
 #ifndef GGNN_PB_AUX
-#define GGNN_PB_AUX 0  // cache policy of k_prop_bwd's dh_in loads
+#define GGNN_PB_AUX kNT  // k_prop_bwd's dh_in loads (read once; -0.9 %)
+#endif
+#ifndef GGNN_PB_DX_NT
+#define GGNN_PB_DX_NT 0  // nontemporal dX^T loads (experiment)
 #endif
 #ifndef GGNN_PROP_A_AUX
 #define GGNN_PROP_A_AUX kNT
@@ -186,7 +189,15 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   for (int s = 0; s < KV; ++s) {
     const Act* p = dXT + wg_off(n, rowg + 16 * s + 8 * hh, H);  // K-blocked (ggnn_common.h)
     if constexpr (SPLIT) {
-      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      f4v a, b;
+      if (GGNN_PB_DX_NT) {
+        a = __builtin_nontemporal_load((const f4v*)p);
+        b = __builtin_nontemporal_load((const f4v*)(p + 4));
+      } else {
+        a = *(const f4v*)p;
+        b = *(const f4v*)(p + 4);
+      }
       const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       dxh[s] = pk8<true>(x);
       dxl[s] = pk8_lo<true>(x);
