@@ -27,7 +27,7 @@ EXPORTED = (
     "ggnn_set_adjacency_edges",
     "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_heads_workspace_bytes",
-    "ggnn_heads_forward", "ggnn_heads_backward", "ggnn_dbg_gemm",
+    "ggnn_heads_forward", "ggnn_heads_backward", "ggnn_dbg_gemm", "ggnn_dbg_gemm_ex",
 )
 NUM_KERNEL_KINDS = 11
 
@@ -105,6 +105,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_heads_backward.argtypes = [_DP, _P, _I, _P, _P, F, _P, _P, _P, _P, _P]
         lib.ggnn_dbg_gemm.restype = _I
         lib.ggnn_dbg_gemm.argtypes = [_DP, _I, _I, _I, _P, _P, _P, _P]
+        lib.ggnn_dbg_gemm_ex.restype = _I
+        lib.ggnn_dbg_gemm_ex.argtypes = [_DP, _I, _I, _I, _P, _I, _P, _I, _P, _I, _P]
         lib.ggnn_kernel_kind_name.restype = ctypes.c_char_p
         lib.ggnn_kernel_kind_name.argtypes = [_I]
         lib.ggnn_profile_begin.restype = _I

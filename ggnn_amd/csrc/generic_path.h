@@ -79,12 +79,74 @@ GemmArgs gg_args() {
   return a;
 }
 
+// k_gemm_ring (k_gemm_ring.h) takes a product when every 16-byte DMA chunk of
+// its operands is a whole, aligned piece of one operand row: 16-byte aligned
+// bases, the non-unit strides multiples of a chunk (4 fp32 / 8 u16), the
+// contiguous extent (K, or the rows of a row-contiguous operand) inside its
+// stride.  Everything else (odd hidden sizes, o = 150 head rows, the
+// transposed adjacency) runs on k_gemm.
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool ring_ok(const GemmArgs& a, bool A16, bool AKC, bool BKC) {
+  if (A16 && !AKC) return false;
+  const long va = A16 ? 8 : 4;
+  if (!al16(a.A) || (a.A2 && !al16(a.A2)) || (a.Am2 && !al16(a.Am2)) || !al16(a.B)) return false;
+  if (a.sAp % va || a.sAq % va || a.sBp % 4 || a.sBq % 4) return false;
+  // k-contiguous fp32 operands: whole chunks up to K (and up to every split-K
+  // chunk's end); 16-bit: zeros from K to the next multiple of 8 (the caller's
+  // padding)
+  const bool kc4 = a.K % 4 == 0 && (a.Ktot == a.K || (a.Ktot % 4 == 0 && a.sKp % 4 == 0));
+  if ((AKC && !A16 && !kc4) || (BKC && !kc4)) return false;
+  if (AKC) {
+    if (a.sAk != 1 || a.sAm % va || (a.M > 1 && a.K > a.sAm)) return false;
+  } else {
+    const long rows = a.Msplit ? std::max<long>(a.Msplit, a.M - a.Msplit) : a.M;
+    if (a.sAm != 1 || a.sAk % 4 || a.Msplit % 4 || (a.K > 1 && rows > a.sAk)) return false;
+  }
+  if (BKC) {
+    if (a.sBk != 1 || a.sBn % 4 || (a.N > 1 && a.K > a.sBn)) return false;
+  } else {
+    if (a.sBn != 1 || a.sBk % 4 || (a.K > 1 && a.N > a.sBk)) return false;
+  }
+  return true;
+}
+// ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail)
+static int g_gemm_force = 0;
+// GGNN_GEMM_KERNEL=old forces k_gemm everywhere (A/B measurements)
+static int gemm_kernel_env() {
+  static const int v = [] {
+    const char* e = getenv("GGNN_GEMM_KERNEL");
+    return (e && !strcmp(e, "old")) ? 1 : 0;
+  }();
+  return v;
+}
+
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
 template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
+  if ((g_gemm_force == 2 || (g_gemm_force == 0 && gemm_kernel_env() == 0)) && ring_ok(a, A16, AKC, BKC)) {
+    const int tn = (a.N + 127) / 128, tm = (a.M + 127) / 128;
+    const long nwg = (long)tn * tm * a.Z;
+    if (nwg > 0x7fffffffL) return fail(GGNN_EINVAL, "k_gemm_ring: grid too large");
+    const dim3 grid((unsigned)nwg);
+    Prof p(kind, s);
+    const bool sc = a.scA != 1.0f || a.scB != 1.0f;
+#define GGR(A16_, AKC_, BKC_)                                                                              \
+  do {                                                                                                       \
+    if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true>), grid, dim3(256), 0, s, a, tm, tn);  \
+    else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false>), grid, dim3(256), 0, s, a, tm, tn);    \
+  } while (0)
+    if (A16 && !BKC) GGR(true, true, false);
+    else if (A16) return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
+    else if (AKC && !BKC) GGR(false, true, false);
+    else if (AKC && BKC) GGR(false, true, true);
+    else if (!AKC && !BKC) GGR(false, false, false);
+    else return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
+#undef GGR
+    return GGNN_OK;
+  }
   // 64 x 64 block tiles: measured faster than the 128 x 64 / 128 x 128
   // variants of k_gemm on every shape tried (tools/gemm_probe.py: 4096^3, the
   // heads' 32768 x {150, 512} x {512, 150, 256}, a per-graph 128 x 256 x 256):

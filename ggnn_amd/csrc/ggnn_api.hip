@@ -21,6 +21,7 @@
 #include "k_wgrad.h"
 #include "k_head.h"
 #include "k_gemm.h"
+#include "k_gemm_ring.h"
 #include "k_generic.h"
 
 // ---------------------------------------------------------------------------
@@ -992,6 +993,34 @@ int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const
     case PREC_F16: return gg_launch<PREC_F16>(a, false, true, false, K_PROP_FWD, s);
     default: return gg_launch<PREC_BF16>(a, false, true, false, K_PROP_FWD, s);
   }
+}
+
+int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int a_layout, const float* B,
+                     int b_layout, float* D, int kernel, ggnn_stream_t stream) {
+  Cfg c;
+  if (int e = make_cfg(d, &c)) return e;
+  if (!A || !B || !D || M < 1 || N < 1 || K < 1 || a_layout < 0 || a_layout > 2 || b_layout < 0 || b_layout > 1 ||
+      kernel < 0 || kernel > 2)
+    return fail(GGNN_EINVAL, "dbg_gemm_ex: bad arguments");
+  GemmArgs a = gg_args();
+  const bool akc = a_layout != 1, a16 = a_layout == 2, bkc = b_layout == 1;
+  a.A = A;
+  if (akc) { a.sAm = K; a.sAk = 1; } else { a.sAm = 1; a.sAk = M; }
+  a.B = B;
+  if (bkc) { a.sBn = K; a.sBk = 1; } else { a.sBn = 1; a.sBk = N; }
+  a.D = D; a.sDm = N; a.sDn = 1;
+  a.M = M; a.N = N; a.K = K;
+  if (kernel == 2 && !ring_ok(a, a16, akc, bkc)) return fail(GGNN_EINVAL, "dbg_gemm_ex: operands not ring-aligned");
+  hipStream_t s = (hipStream_t)stream;
+  g_gemm_force = kernel;
+  int e;
+  switch (c.prec) {
+    case PREC_SPLIT: e = gg_launch<PREC_SPLIT>(a, a16, akc, bkc, K_PROP_FWD, s); break;
+    case PREC_F16: e = gg_launch<PREC_F16>(a, a16, akc, bkc, K_PROP_FWD, s); break;
+    default: e = gg_launch<PREC_BF16>(a, a16, akc, bkc, K_PROP_FWD, s); break;
+  }
+  g_gemm_force = 0;
+  return e;
 }
 
 // ---- embedding front-end and output heads (k_head.h)

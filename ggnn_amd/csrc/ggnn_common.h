@@ -68,10 +68,24 @@ template <bool F16> DEV float from_limb(u16 x) {
 }
 // residual of the limb rounding of x
 template <bool F16> DEV float lo_part(float x) { return x - from_limb<F16>(to_limb<F16>(x)); }
+// pairs through the packed converts (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32:
+// one instruction per pair, round to nearest even like the scalar casts)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 template <bool F16> DEV uint32_t pk(float a, float b) {
-  return (uint32_t)to_limb<F16>(a) | ((uint32_t)to_limb<F16>(b) << 16);
+  const f32x2v v = {a, b};
+  if constexpr (F16) return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));
+  else return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
 }
-template <bool F16> DEV uint32_t pk_lo(float a, float b) { return pk<F16>(lo_part<F16>(a), lo_part<F16>(b)); }
+template <bool F16> DEV uint32_t pk_lo(float a, float b) {
+  const f32x2v v = {a, b};
+  f32x2v back;
+  if constexpr (F16) back = __builtin_convertvector(__builtin_convertvector(v, f16x2v), f32x2v);
+  else back = __builtin_convertvector(__builtin_convertvector(v, bf16x2v), f32x2v);
+  const f32x2v lo = v - back;
+  return pk<F16>(lo.x, lo.y);
+}
 template <bool F16> DEV frag pk8(const float* x) {
   return make_uint4(pk<F16>(x[0], x[1]), pk<F16>(x[2], x[3]), pk<F16>(x[4], x[5]), pk<F16>(x[6], x[7]));
 }
@@ -168,6 +182,18 @@ DEV void glds_tile(char* lds, const u16* src, int tid) {
                                        (__attribute__((address_space(3))) void*)(lds + qb * 16), 16, 0, AUX);
     }
   }
+}
+
+// LDS-DMA of 16 B per lane in inline asm: invisible to hipcc's waitcnt pass,
+// which would otherwise wait vmcnt(0) before every ds_read of the ring (it
+// cannot tell the ring slots apart); completion is counted by hand below.
+DEV void glds16_asm(const void* gsrc, const char* lds_dst) {
+  unsigned keep;
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
 }
 
 // B-operand fragment of a packed matrix: [strip][kstep][64 lanes][8] limbs

@@ -1,0 +1,288 @@
+// k_gemm_ring.h -- the general path's product kernel for aligned operands
+// (same GemmArgs contract as k_gemm, k_gemm.h).
+//
+// k_gemm stages every 64 x 32 operand slice through VGPRs with one slice in
+// flight per workgroup; at 4096^3 it reached 115 TFLOP/s in the split mode
+// and 107 in bf16 (tools/gemm_probe.py): latency-bound on its operand reads,
+// not on the MFMAs.  This kernel instead:
+//   * takes 128 x 128 block tiles (4 waves in 2 x 2, 64 x 64 outputs each:
+//     four v_mfma_f32_32x32x16 accumulators), half the operand bytes per flop;
+//   * DMAs raw operand K-slices (fp32, or the exact 16-bit adjacency) straight
+//     into a 4-slot LDS ring with global_load_lds_dwordx4 -- three slices in
+//     flight, no VGPR staging, completion counted by hand (vmcnt + s_barrier);
+//   * converts on the LDS -> register path: each wave reads its fragments'
+//     8 fp32 values and forms the precision policy's limbs (split: f16 hi/lo)
+//     right before the MFMAs, so there is no second LDS image and one barrier
+//     per slice.
+// Out-of-range rows / k cost no branches in the MFMA loop: row addresses are
+// clamped into the operand (their outputs are discarded), and a chunk whose k
+// lies past the term's K is DMA'd from a zero block instead, so both operands
+// carry zeros there.  K is a multiple of the chunk (4 fp32) for fp32
+// k-contiguous operands; a 16-bit operand's columns between K and the next
+// multiple of 8 must hold zeros (the staged adjacency's padding does).
+//
+// Slice images (one ring slot = A image, then B image):
+//   k-contiguous fp32  [128 rows][32 k]: 128 B rows, 16-B chunk c of row r at
+//                      slot c ^ ((r >> 1) & 7) -- 16 consecutive rows of one
+//                      fragment read hit 16 distinct 4-bank groups;
+//   k-contiguous u16   [128 rows][32 k]: 64 B rows, chunk c at c ^ ((r >> 2) & 3);
+//   row-contiguous fp32 [32 k][128 rows]: 512 B k-rows, chunk c (4 rows) at
+//                      c ^ (8 * ((k >> 3) & 1)) -- the two lane halves of a
+//                      fragment (k and k + 8) read opposite bank halves.
+#pragma once
+#include "k_gemm.h"
+
+__device__ __attribute__((aligned(16))) const float g_ring_zero[4] = {0.f, 0.f, 0.f, 0.f};
+
+namespace gr {
+constexpr int BM = 128, BN = 128, BK = 32, NBUF = 4, NT = 256;
+
+DEV int kc32_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+DEV int kc16_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); }
+DEV int rc32_off(int kr, int r) { return kr * 512 + (((r >> 2) ^ (((kr >> 3) & 1) << 3)) << 4) + ((r & 3) << 2); }
+
+// 8 fp32 of image row r at k0 .. k0 + 7 (k0 a multiple of 8)
+template <bool KC>
+DEV void rd8(const char* img, int r, int k0, float* x) {
+  if constexpr (KC) {
+    const int c = k0 >> 2;
+    const float4 p = *(const float4*)(img + kc32_off(r, c));
+    const float4 q = *(const float4*)(img + kc32_off(r, c + 1));
+    x[0] = p.x; x[1] = p.y; x[2] = p.z; x[3] = p.w;
+    x[4] = q.x; x[5] = q.y; x[6] = q.z; x[7] = q.w;
+  } else {
+    const char* b = img + rc32_off(k0, r);  // (k0 >> 3) & 1 is the same for k0 .. k0 + 7
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = *(const float*)(b + j * 512);
+  }
+}
+}  // namespace gr
+
+// blockIdx.x -> (z, m tile, n tile): consecutive dispatch ids go round-robin
+// over the 8 XCDs (private L2 each), so ids are first remapped bijectively
+// (guide T1) to give every XCD a contiguous run of the logical order, and the
+// logical order walks groups of GM m-tiles with n fastest inside a group: the
+// ~32 tiles an XCD holds at once share a few A row-panels and B column-panels.
+DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
+  const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per = tm * tn;
+  z = lin / per;
+  const int t = lin - z * per;
+  constexpr int GM = 4;
+  const int g = t / (GM * tn), m0 = g * GM, gs = min(tm - m0, GM);
+  const int u = t - g * GM * tn;
+  mt = m0 + u % gs;
+  nt = u / gs;
+}
+
+template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE>
+__global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
+  using namespace gr;
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  static_assert(!A16 || AKC, "16-bit A operands are k-contiguous");
+  constexpr int ES = A16 ? 2 : 4;                       // A element bytes
+  constexpr int AB = A16 ? BM * BK * 2 : BM * BK * 4;  // A slice image bytes
+  constexpr int BB = BN * BK * 4;
+  constexpr int SB = AB + BB;
+  constexpr int GA = AB / 1024 / 4, GB = BB / 1024 / 4;  // DMA instructions per wave per slice
+  constexpr int GPW = GA + GB;
+  // one __shared__ object per ring slot, addressed with compile-time indices
+  __shared__ __attribute__((aligned(16))) char s0[SB], s1[SB], s2[SB], s3[SB];
+  auto slot = [&](int u) -> char* { return u == 0 ? s0 : u == 1 ? s1 : u == 2 ? s2 : s3; };
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int wm = w & 1, wn = w >> 1;
+  int z, mt, ntile;
+  ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  if (z >= a.Z) return;
+  if (a.zmask && !a.zmask[z]) return;
+  const int n0 = ntile * BN, m0 = mt * BM;
+  const int kc = (a.K + BK - 1) / BK;
+  const int zp = z / a.zdiv, zq = z % a.zdiv;
+  const int nterms = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
+  const int nit = nterms * kc;
+  // z's first 128 terms in two VGPRs (lane l: terms l and 64 + l), fetched
+  // by v_readlane: a global or LDS read of the list inside the ring would come
+  // with a vmcnt(0) wait that drains the DMAs in flight
+  int tl0 = 0, tl1 = 0;
+  if (a.tl) {
+    const int* tz = a.tl + (long)z * a.ts + 1;
+    if (lane < nterms) tl0 = tz[lane];
+    if (64 + lane < nterms) tl1 = tz[64 + lane];
+  }
+  asm volatile("" : "+v"(tl0), "+v"(tl1));  // the loads' wait goes here, before the ring
+  const int keff = (int)min((long)a.K, a.Ktot - (long)zp * a.sKp);  // valid k of every term of z
+
+  // ---- per-lane DMA source of every chunk this wave moves, at the term's
+  // k = 0 (rebuilt when a new term starts); a slice adds kk0 * kstep
+  const char* pa[GA];
+  const char* pb[GB];
+  int ka[GA], kb[GB];  // chunk k offset inside the slice (KC) or k-row (row-contiguous)
+  auto term_bases = [&](int e) {
+    const int q = !a.tl ? zq + e
+                  : e < 64 ? __builtin_amdgcn_readlane(tl0, e)
+                  : e < 128 ? __builtin_amdgcn_readlane(tl1, e - 64)
+                            : a.tl[(long)z * a.ts + 1 + e];
+    const bool second = a.A2 && q == 1;
+    const long abase = (long)zp * a.sAp + (second ? 0 : (long)q * a.sAq);
+    const char* A1 = (const char*)(second ? a.A2 : a.A);
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const int qs = (g * 4 + w) * 64 + lane;
+      int row;
+      if constexpr (A16) {
+        row = qs >> 2;
+        ka[g] = ((qs & 3) ^ ((row >> 2) & 3)) << 3;
+      } else if constexpr (AKC) {
+        row = qs >> 3;
+        ka[g] = ((qs & 7) ^ ((row >> 1) & 7)) << 2;
+      } else {
+        ka[g] = qs >> 5;
+        row = ((qs & 31) ^ (((ka[g] >> 3) & 1) << 3)) << 2;
+      }
+      int mg = m0 + row;
+      const char* P = A1;
+      int lim = a.Msplit ? a.Msplit : a.M;
+      if (a.Msplit && mg >= a.Msplit) {
+        P = (const char*)a.Am2;
+        mg -= a.Msplit;
+        lim = a.M - a.Msplit;
+      }
+      mg = AKC ? min(mg, lim - 1) : min(mg, (lim - 1) & ~3);
+      pa[g] = P + (abase + (long)mg * a.sAm) * ES;
+    }
+    const long bbase = (long)zp * a.sBp + (long)q * a.sBq;
+#pragma unroll
+    for (int g = 0; g < GB; ++g) {
+      const int qs = (g * 4 + w) * 64 + lane;
+      int row;
+      if constexpr (BKC) {
+        row = qs >> 3;
+        kb[g] = ((qs & 7) ^ ((row >> 1) & 7)) << 2;
+        row = min(n0 + row, a.N - 1);
+      } else {
+        kb[g] = qs >> 5;
+        row = min(n0 + (((qs & 31) ^ (((kb[g] >> 3) & 1) << 3)) << 2), (a.N - 1) & ~3);
+      }
+      pb[g] = (const char*)a.B + (bbase + (long)row * a.sBn) * 4;
+    }
+  };
+
+  // ---- DMA of slice `it` (term it / kc, k offset (it % kc) * BK) into ring slot `buf`
+  auto stage = [&](int it, char* buf) {
+    const int j = it % kc, kk0 = j * BK;
+    if (j == 0) term_bases(it / kc);
+    const char* zero = (const char*)g_ring_zero;
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const int k = kk0 + ka[g];
+      const char* src = AKC ? pa[g] + (long)k * ES : pa[g] + (long)k * a.sAk * 4;
+      glds16_asm(k < keff ? src : zero, buf + (g * 4 + w) * 1024);
+    }
+#pragma unroll
+    for (int g = 0; g < GB; ++g) {
+      const int k = kk0 + kb[g];
+      const char* src = BKC ? pb[g] + (long)k * 4 : pb[g] + (long)k * a.sBk * 4;
+      glds16_asm(k < keff ? src : zero, buf + AB + (g * 4 + w) * 1024);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = splat(0.f);
+
+  // ---- MFMAs of the slice in ring slot `buf` (straight-line: the LDS reads
+  // of both k-steps issue together)
+  auto compute = [&](const char* buf) {
+    const char* ia = buf;
+    const char* ib = buf + AB;
+    const float sa = a.scA, sb = a.scB;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int k0 = 16 * s + 8 * hh;
+      frag ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 64 + i * 32 + l32;
+        if constexpr (A16) {
+          ah[i] = *(const frag*)(ia + kc16_off(r, k0 >> 3));
+          al[i] = ah[i];
+        } else {
+          float x[8];
+          rd8<AKC>(ia, r, k0, x);
+          if constexpr (SCALE)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) x[t] *= sa;
+          ah[i] = pk8<F16>(x);
+          al[i] = SPLIT ? pk8_lo<true>(x) : ah[i];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + j * 32 + l32;
+        float x[8];
+        rd8<BKC>(ib, r, k0, x);
+        if constexpr (SCALE)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) x[t] *= sb;
+        bh[j] = pk8<F16>(x);
+        bl[j] = SPLIT ? pk8_lo<true>(x) : bh[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (A16) mma_xa<PREC>(acc[i][j], ah[i], bh[j], bl[j]);
+          else mma<PREC>(acc[i][j], ah[i], al[i], bh[j], bl[j]);
+        }
+    }
+  };
+
+  // ---- the ring: slices it+1, it+2 stay in flight while slice it is consumed
+#pragma unroll
+  for (int u = 0; u < NBUF - 1; ++u)
+    if (u < nit) stage(u, slot(u));
+  for (int it0 = 0; it0 < nit; it0 += NBUF) {
+#pragma unroll
+    for (int u = 0; u < NBUF; ++u) {
+      const int it = it0 + u;
+      if (it < nit) {
+        if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+        else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
+        if (it + NBUF - 1 < nit) stage(it + NBUF - 1, slot((u + NBUF - 1) % NBUF));
+        compute(slot(u));
+      }
+    }
+  }
+
+  // ---- epilogue (as k_gemm)
+  const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
+  const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + 32 * j + l32;
+    if (n >= a.N) continue;
+    const float bn = bias ? bias[n] : 0.f;
+    const bool hi_n = a.Nsplit && n >= a.Nsplit;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + acc_row(r, hh);
+        if (m >= a.M) continue;
+        float x = a.alpha * acc[i][j][r] + bn;
+        if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
+        else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+        const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+        if (a.E) x *= a.E[doff];
+        float* d = (hi_n ? a.D2 : a.D) + doff;
+        if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+        else if (a.mode == GG_ADD) *d += x;
+        else *d = x;
+      }
+  }
+}

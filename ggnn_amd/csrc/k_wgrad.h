@@ -159,18 +159,6 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
 // the DMAs every step).  16-bit operands only (the split mode's weight-gradient
 // operands are single f16 limbs).
 // ===========================================================================
-// LDS-DMA of 16 B per lane in inline asm: invisible to hipcc's waitcnt pass,
-// which would otherwise wait vmcnt(0) before every ds_read of the ring (it
-// cannot tell the ring slots apart); completion is counted by hand below.
-DEV void glds16_asm(const void* gsrc, const char* lds_dst) {
-  unsigned keep;
-  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(dst)
-               : "memory");
-}
-
 template <int PREC>
 __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   constexpr bool F16 = Prec<PREC>::f16;

@@ -139,6 +139,15 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack,
 int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const float* B, float* D,
                   ggnn_stream_t stream);
 
+/* The same with every operand layout the general path uses:
+ *   a_layout 0: A fp32 [M][K]; 1: A fp32 [K][M]; 2: A 16-bit limbs [M][K]
+ *               (exact values: 0/1 adjacency; f16 in the fp16 / fp32 modes)
+ *   b_layout 0: B fp32 [K][N]; 1: B fp32 [N][K]
+ *   kernel   0: automatic; 1: k_gemm; 2: k_gemm_ring (GGNN_EINVAL if the
+ *               operands do not meet its alignment rules) */
+int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int a_layout, const float* B,
+                     int b_layout, float* D, int kernel, ggnn_stream_t stream);
+
 /* Stage one batch's adjacency [b][C][v][v] fp32 (0/1) into `adj` (sized by
  * ggnn_adjacency_bytes): 16-bit (exact for 0/1; bf16, or f16 under GGNN_FP16 /
  * GGNN_FP32_PARITY), its transpose, per-node in-degrees and the per-graph list

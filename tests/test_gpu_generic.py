@@ -169,3 +169,54 @@ def test_k_gemm_against_numpy(M, N, K, precision):
     scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
     err = float(np.max(np.abs(got - ref) / np.maximum(scale, 1e-30)))
     assert err <= {"fp32": 1e-6, "fp16": 2e-3, "bf16": 1e-2}[precision], err
+
+
+def _gemm_ex(A, a_layout, B, b_layout, M, N, K, precision, kernel):
+    torch = _torch()
+    import ctypes
+    from ggnn_amd import _lib
+    dev = torch.device("cuda", 0)
+    a, b = torch.from_numpy(np.ascontiguousarray(A)).to(dev), torch.from_numpy(np.ascontiguousarray(B)).to(dev)
+    d = torch.full((M, N), float("nan"), device=dev)
+    dims = _lib.dims(1, 1, 64, 1, 1, True, precision)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.load().ggnn_dbg_gemm_ex(ctypes.byref(dims), M, N, K, ctypes.c_void_p(a.data_ptr()), a_layout,
+                                            ctypes.c_void_p(b.data_ptr()), b_layout, ctypes.c_void_p(d.data_ptr()),
+                                            kernel, s), "ggnn_dbg_gemm_ex")
+    return d.cpu().numpy()
+
+
+# (M, N multiples of 4 and K of 8: the ring's alignment rules for every layout
+# below; ragged against its 128 x 128 tiles and 32-wide K slices)
+RING_SHAPES = [(4, 4, 8), (128, 128, 32), (132, 260, 40), (400, 800, 400), (28, 400, 88), (1000, 48, 1000),
+               (64, 128, 8), (36, 36, 200)]
+
+
+@pytest.mark.parametrize("M,N,K", RING_SHAPES)
+@pytest.mark.parametrize("a_layout,b_layout", [(0, 0), (0, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_k_gemm_ring_layouts(M, N, K, a_layout, b_layout, precision):
+    """k_gemm_ring (128 x 128 tiles, LDS-DMA ring) on every operand layout the
+    general path uses, incl. ragged M / N / K tails and K < one slice: fp32
+    mode within 1e-6 of float64 relative to the accumulated magnitude, and
+    identical to k_gemm's result up to accumulation order."""
+    rng = np.random.default_rng(M * 7 + N * 3 + K)
+    if a_layout == 2:   # exact 16-bit operand (the 0/1 adjacency)
+        A = (rng.random((M, K)) < 0.3).astype(np.float32)
+        Aop = A.astype(np.float16).view(np.uint16) if precision != "bf16" else (A.view(np.uint32) >> 16).astype(np.uint16)
+    else:
+        A = rng.standard_normal((M, K)).astype(np.float32)
+        Aop = A if a_layout == 0 else np.ascontiguousarray(A.T)
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    Bop = B if b_layout == 0 else np.ascontiguousarray(B.T)
+    ring = _gemm_ex(Aop, a_layout, Bop, b_layout, M, N, K, precision, 2)
+    old = _gemm_ex(Aop, a_layout, Bop, b_layout, M, N, K, precision, 1)
+    ref = A.astype(np.float64) @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+    # (plus an absolute floor of 2^-24 per term: the f16 lo limb of an operand
+    # below 2^-3 in magnitude is subnormal, in both kernels alike)
+    tol = {"fp32": 1e-6, "bf16": 1e-2}[precision]
+    bound = tol * scale + K * 2.0 ** -24
+    for got in (ring, old):
+        assert np.all(np.abs(got - ref) <= bound), float(np.max(np.abs(got - ref) / bound))
+    assert np.all(np.abs(ring - old) <= 2 * bound)
