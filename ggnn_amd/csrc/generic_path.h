@@ -17,17 +17,28 @@
 #pragma once
 
 struct GenAdjL {
-  size_t Ag, occ, chl, cgl, total;
+  size_t Ag, AgT, occ, chl, cgl, cgc, total;
   int vp;
+  int nch, gch;  // cgc: every channel's graph list cut into nch chunks of <= gch graphs
 };
 GenAdjL gen_adj_layout(const Cfg& c) {
   GenAdjL L;
   size_t o = 0;
   L.vp = (c.vin + 7) & ~7;
+  // dW_c = sum over c's graphs of h^T dM: one workgroup per (channel, 128 x
+  // 128 output tile) would leave most CUs idle (8 channels x 16 tiles at
+  // hidden 400); chunks of the graph list as separate z (fp32 atomics) give
+  // about 2048 workgroups
+  const int tiles = ((c.H + 127) / 128) * ((c.H + 127) / 128);
+  L.nch = std::max(1, std::min(c.b, (2048 + c.C * tiles - 1) / (c.C * tiles)));
+  L.gch = (c.b + L.nch - 1) / L.nch;
+  L.nch = (c.b + L.gch - 1) / L.gch;
   L.Ag = o;  o += al((size_t)c.b * c.C * c.vin * L.vp * 2);
+  L.AgT = o; o += al((size_t)c.b * c.C * c.vin * L.vp * 2);
   L.occ = o; o += al((size_t)c.b * c.C);
   L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);
   L.cgl = o; o += al((size_t)c.C * (c.b + 1) * 4);
+  L.cgc = o; o += al((size_t)c.C * L.nch * (L.gch + 1) * 4);
   L.total = o;
   return L;
 }
@@ -120,6 +131,19 @@ static int gemm_kernel_env() {
   return v;
 }
 
+// ring depth: 2 slots (64 KiB: two workgroups per CU) by default -- measured
+// 1.4-2x faster than the 4-slot ring (one workgroup per CU) on every probe
+// shape (tools/gemm_ring_probe.py): a second workgroup's MFMAs cover one's
+// prologue, barriers and epilogue better than deeper prefetch does;
+// GGNN_RING_NBUF=4 selects the 4-slot ring
+static int ring_nbuf_env() {
+  static const int v = [] {
+    const char* e = getenv("GGNN_RING_NBUF");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
 template <int PREC>
@@ -133,10 +157,13 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     const dim3 grid((unsigned)nwg);
     Prof p(kind, s);
     const bool sc = a.scA != 1.0f || a.scB != 1.0f;
+    const bool nb2 = ring_nbuf_env() == 2;
 #define GGR(A16_, AKC_, BKC_)                                                                              \
   do {                                                                                                       \
-    if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true>), grid, dim3(256), 0, s, a, tm, tn);  \
-    else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false>), grid, dim3(256), 0, s, a, tm, tn);    \
+    if (sc && nb2) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2>), grid, dim3(256), 0, s, a, tm, tn); \
+    else if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 4>), grid, dim3(256), 0, s, a, tm, tn); \
+    else if (nb2) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2>), grid, dim3(256), 0, s, a, tm, tn); \
+    else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 4>), grid, dim3(256), 0, s, a, tm, tn);    \
   } while (0)
     if (A16 && !BKC) GGR(true, true, false);
     else if (A16) return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
@@ -171,10 +198,10 @@ int gen_set_adjacency(const Cfg& c, void* adj, const float* A, hipStream_t s) {
   Prof p(K_ADJ, s);
   if (c.prec == PREC_BF16)
     hipLaunchKernelGGL(k_gen_adj<false>, dim3((unsigned)(c.b * c.C)), dim3(256), 0, s, A, c.vin, L.vp,
-                       P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+                       P<u16>(adj, L.Ag), P<u16>(adj, L.AgT), P<unsigned char>(adj, L.occ));
   else
     hipLaunchKernelGGL(k_gen_adj<true>, dim3((unsigned)(c.b * c.C)), dim3(256), 0, s, A, c.vin, L.vp,
-                       P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+                       P<u16>(adj, L.Ag), P<u16>(adj, L.AgT), P<unsigned char>(adj, L.occ));
   return GGNN_OK;
 }
 int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const int32_t* goff, int64_t ne, int E,
@@ -182,10 +209,12 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
   const GenAdjL L = gen_adj_layout(c);
   Prof p(K_ADJ, s);
   HIPCHK(hipMemsetAsync(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s));
+  HIPCHK(hipMemsetAsync(P<u16>(adj, L.AgT), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s));
   HIPCHK(hipMemsetAsync(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C, s));
   if (ne > 0)
     hipLaunchKernelGGL(k_gen_adj_edges, dim3((unsigned)std::min(c.b, 4096)), dim3(256), 0, s, edges, goff, c.b, c.vin,
-                       L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<unsigned char>(adj, L.occ));
+                       L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<u16>(adj, L.AgT),
+                       P<unsigned char>(adj, L.occ));
   return GGNN_OK;
 }
 // channel lists of the staged batch (per graph, per channel); rebuilt by every
@@ -194,7 +223,8 @@ void gen_lists(const Cfg& c, void* adj, hipStream_t s) {
   const GenAdjL L = gen_adj_layout(c);
   const int n = c.b + c.C;
   hipLaunchKernelGGL(k_gen_lists, dim3((n + 255) / 256), dim3(256), 0, s, P<const unsigned char>(adj, L.occ), c.b,
-                     c.C, (c.flags & GGNN_DENSE_CHANNELS) ? 1 : 0, P<int>(adj, L.chl), P<int>(adj, L.cgl));
+                     c.C, (c.flags & GGNN_DENSE_CHANNELS) ? 1 : 0, P<int>(adj, L.chl), P<int>(adj, L.cgl),
+                     P<int>(adj, L.cgc), L.nch, L.gch);
 }
 
 // -------------------------------------------------------------------- forward
@@ -356,12 +386,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // dM[g,c] = A[g,c]^T dX[g] over the non-empty tiles
     {
       GemmArgs a = gg_args();
-      a.A = P<u16>(adj, AL.Ag); a.sAp = C * v * AL.vp; a.sAq = v * AL.vp; a.sAm = 1; a.sAk = AL.vp;
+      a.A = P<u16>(adj, AL.AgT); a.sAp = C * v * AL.vp; a.sAq = v * AL.vp; a.sAm = AL.vp; a.sAk = 1;
       a.B = DXH; a.sBp = v * 2 * H; a.sBk = 2 * H; a.sBn = 1;
       a.D = dM; a.sDz = v * H; a.sDm = H; a.sDn = 1;
       a.zdiv = (int)C; a.Z = (int)(c.b * C); a.zmask = dense_ch ? nullptr : P<unsigned char>(adj, AL.occ);
       a.M = (int)v; a.N = (int)H; a.K = (int)v;
-      if (int e = gg_launch<PREC>(a, true, false, false, K_PROP_BWD, s)) return e;
+      if (int e = gg_launch<PREC>(a, true, true, false, K_PROP_BWD, s)) return e;
     }
     // dh[g] += sum over g's channels of dM[g,c] W_c^T
     {
@@ -376,12 +406,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // dW_c (+)= sum over c's graphs of h_t[g]^T dM[g,c]; dbeta_c += column sums of dM[g,c]
     {
       float* G_out = c.ed ? P<float>(ws, L.GW) : dW;
+      const bool chunked = AL.nch > 1;
+      if (chunked && c.ed) HIPCHK(hipMemsetAsync(G_out, 0, (size_t)C * H * H * 4, s));
       GemmArgs a = gg_args();
       a.A = ht; a.sAq = v * H; a.sAm = 1; a.sAk = H;
       a.B = dM; a.sBp = v * H; a.sBq = C * v * H; a.sBk = H; a.sBn = 1;
-      a.D = G_out; a.sDz = H * H; a.sDm = H; a.sDn = 1; a.mode = c.ed ? GG_STORE : GG_ADD;
-      a.tl = P<int>(adj, AL.cgl); a.ts = c.b + 1;
-      a.Z = (int)C; a.M = (int)H; a.N = (int)H; a.K = (int)v;
+      a.D = G_out; a.sDp = H * H; a.sDm = H; a.sDn = 1;
+      a.mode = chunked ? GG_ATOMIC : c.ed ? GG_STORE : GG_ADD;
+      a.tl = P<int>(adj, AL.cgc); a.ts = AL.gch + 1; a.zdiv = AL.nch;  // z = (channel, chunk of its graphs)
+      a.Z = (int)C * AL.nch; a.M = (int)H; a.N = (int)H; a.K = (int)v;
       if (int e = gg_launch<PREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       if (c.ed)

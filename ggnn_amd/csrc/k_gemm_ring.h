@@ -8,8 +8,10 @@
 //   * takes 128 x 128 block tiles (4 waves in 2 x 2, 64 x 64 outputs each:
 //     four v_mfma_f32_32x32x16 accumulators), half the operand bytes per flop;
 //   * DMAs raw operand K-slices (fp32, or the exact 16-bit adjacency) straight
-//     into a 4-slot LDS ring with global_load_lds_dwordx4 -- three slices in
-//     flight, no VGPR staging, completion counted by hand (vmcnt + s_barrier);
+//     into an LDS ring with global_load_lds_dwordx4 -- no VGPR staging,
+//     completion counted by hand (vmcnt + s_barrier).  Two slots (64 KiB, two
+//     workgroups per CU) measured 1.4-2x faster than four slots (three slices
+//     in flight, one workgroup per CU);
 //   * converts on the LDS -> register path: each wave reads its fragments'
 //     8 fp32 values and forms the precision policy's limbs (split: f16 hi/lo)
 //     right before the MFMAs, so there is no second LDS image and one barrier
@@ -35,7 +37,7 @@
 __device__ __attribute__((aligned(16))) const float g_ring_zero[4] = {0.f, 0.f, 0.f, 0.f};
 
 namespace gr {
-constexpr int BM = 128, BN = 128, BK = 32, NBUF = 4, NT = 256;
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 
 DEV int kc32_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 DEV int kc16_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); }
@@ -76,7 +78,7 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
   nt = u / gs;
 }
 
-template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE>
+template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF>
 __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -88,7 +90,10 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   constexpr int GA = AB / 1024 / 4, GB = BB / 1024 / 4;  // DMA instructions per wave per slice
   constexpr int GPW = GA + GB;
   // one __shared__ object per ring slot, addressed with compile-time indices
-  __shared__ __attribute__((aligned(16))) char s0[SB], s1[SB], s2[SB], s3[SB];
+  // (NBUF = 4: three slices in flight, one workgroup per CU; NBUF = 2: one
+  // slice in flight, 64 KiB, two workgroups per CU)
+  static_assert(NBUF == 2 || NBUF == 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) char s0[SB], s1[SB], s2[NBUF > 2 ? SB : 16], s3[NBUF > 2 ? SB : 16];
   auto slot = [&](int u) -> char* { return u == 0 ? s0 : u == 1 ? s1 : u == 2 ? s2 : s3; };
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int wm = w & 1, wn = w >> 1;
@@ -249,8 +254,8 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
     for (int u = 0; u < NBUF; ++u) {
       const int it = it0 + u;
       if (it < nit) {
-        if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
-        else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        if (NBUF > 2 && it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+        else if (NBUF > 2 && it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
         if (it + NBUF - 1 < nit) stage(it + NBUF - 1, slot((u + NBUF - 1) % NBUF));

@@ -9,30 +9,35 @@
 #include "ggnn_common.h"
 
 // ---- adjacency staging: A [b][C][v][v] fp32 (0/1) -> Ag [b][C][v][vp] 16-bit
-// limbs (natural order, row pitch vp = v rounded up to 8) and the per-tile
-// occupancy occ[b*C] (1 = the tile holds an edge).  One block per tile.
+// limbs (natural order, row pitch vp = v rounded up to 8, zero padding), its
+// transpose AgT (same layout: the k-contiguous A operand of dM = A^T dX) and
+// the per-tile occupancy occ[b*C] (1 = the tile holds an edge).  One block
+// per tile.
 template <bool F16>
 __global__ void __launch_bounds__(256) k_gen_adj(const float* __restrict__ A, int v, int vp, u16* __restrict__ Ag,
-                                                 unsigned char* __restrict__ occ) {
+                                                 u16* __restrict__ AgT, unsigned char* __restrict__ occ) {
   const long tile = blockIdx.x;
   const float* src = A + tile * (long)v * v;
   u16* dst = Ag + tile * (long)v * vp;
+  u16* dsT = AgT + tile * (long)v * vp;
   int any = 0;
   for (long q = threadIdx.x; q < (long)v * vp; q += 256) {
     const int i = (int)(q / vp), j = (int)(q % vp);
     const float x = j < v ? src[(long)i * v + j] : 0.f;
     any |= x != 0.f;
     dst[q] = to_limb<F16>(x);
+    if (j < v) dsT[(long)j * vp + i] = to_limb<F16>(x);
+    else dsT[q] = 0;  // (row i of AgT, padding column j)
   }
   any = __syncthreads_or(any);
   if (threadIdx.x == 0) occ[tile] = (unsigned char)(any != 0);
 }
 
 // the same from the reference's edge lists (graph_to_adj_mat_bd semantics,
-// k_prep.h k_adj_from_edges): after a memset of Ag and occ
+// k_prep.h k_adj_from_edges): after a memset of Ag, AgT and occ
 __global__ void __launch_bounds__(256) k_gen_adj_edges(const int* __restrict__ edges, const int* __restrict__ goff,
                                                        int b, int v, int vp, int E, int f16, u16* __restrict__ Ag,
-                                                       unsigned char* __restrict__ occ) {
+                                                       u16* __restrict__ AgT, unsigned char* __restrict__ occ) {
   const int C = 2 * E;
   const u16 one = f16 ? (u16)0x3C00 : (u16)0x3F80;
   for (int g = blockIdx.x; g < b; g += gridDim.x) {
@@ -47,6 +52,7 @@ __global__ void __launch_bounds__(256) k_gen_adj_edges(const int* __restrict__ e
       for (int k = 0; k < 4; ++k) {
         const long tile = (long)g * C + ch[k];
         Ag[(tile * v + ro[k]) * vp + co[k]] = one;
+        AgT[(tile * v + co[k]) * vp + ro[k]] = one;
         occ[tile] = 1;
       }
     }
@@ -54,10 +60,10 @@ __global__ void __launch_bounds__(256) k_gen_adj_edges(const int* __restrict__ e
 }
 
 // per-graph channel lists chl[g*(C+1)] = (count, channels...) and per-channel
-// graph lists cgl[c*(b+1)] = (count, graphs...) from occ; with dense != 0
+// graph lists cgl[c*(b+1)] = (count, graphs...) from occ (and cut into chunks, cgc); with dense != 0
 // every tile counts as occupied (GGNN_DENSE_CHANNELS)
 __global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C, int dense, int* __restrict__ chl,
-                            int* __restrict__ cgl) {
+                            int* __restrict__ cgl, int* __restrict__ cgc, int nch, int gch) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < b) {
     int* o = chl + (long)t * (C + 1);
@@ -72,6 +78,13 @@ __global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C,
     for (int g = 0; g < b; ++g)
       if (dense || occ[(long)g * C + c]) o[1 + n++] = g;
     o[0] = n;
+    // the same list in nch chunks of <= gch graphs: cgc[(c*nch + j)*(gch+1)] = (count, graphs...)
+    for (int j = 0; j < nch; ++j) {
+      int* q = cgc + ((long)c * nch + j) * (gch + 1);
+      const int lo = j * gch, cnt = max(0, min(n - lo, gch));
+      q[0] = cnt;
+      for (int e = 0; e < cnt; ++e) q[1 + e] = o[1 + lo + e];
+    }
   }
 }
 
