@@ -228,8 +228,10 @@ def callers_side(dev, b, v, h, reps=10):
     ms_heads = _timed_events(heads_fb, reps)
     flops = 3 * 2 * b * v * 2 * h * (150 + 46)      # logits, dX, dW GEMMs
     return {"embed_fwd_bwd_ms": ms_embed, "heads_fwd_bwd_ms": ms_heads,
-            "heads_gemm_tflops": flops / (ms_heads * 1e-3) / 1e12, "heads_peak_fp32_vector_tflops": 157.3,
-            "note": "fp32 FMA tiles (parity mode of the callers); tables 64/32/96/64 wide, heads o=150 and 46"}
+            "heads_gemm_tflops_algorithmic": flops / (ms_heads * 1e-3) / 1e12,
+            "note": "heads: both heads' logits, d[hT|h0] and dW as one MFMA product each (k_gemm_ring, split f16 "
+                    "limbs = fp32 parity) + softmax / dZ kernels; fwd+bwd incl. weight dropout; tables 64/32/96/64 "
+                    "wide, heads o=150 and 46"}
 
 
 def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10):

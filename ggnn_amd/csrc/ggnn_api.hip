@@ -1099,23 +1099,37 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
 }
 
 namespace {
+// All heads side by side: head i owns columns [off[i], off[i] + o_i) of the
+// concatenated operands (width Ot, each head padded to a multiple of 4 with
+// zeros), so a head set costs ONE logits, one d[hT | h0] and one dW product
+// (two heads one by one: 3 + 3 launches with 128-column tiles over o = 150 and
+// 46, and a read-modify-write pass over dX for the second head).
+constexpr int HEAD_LP = 2048;  // loss partials per head (one per softmax block)
 struct HeadL {
-  size_t Wd[GGNN_MAX_HEADS], S[GGNN_MAX_HEADS], dZ[GGNN_MAX_HEADS], total;
+  int off[GGNN_MAX_HEADS], Ot;
+  size_t W, Sx, bias, Z, dZ, dW, lp, total;
 };
 int head_layout(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, HeadL* L, const char* what) {
   if (int e = plain_dims(d, what)) return e;
   if (!heads || nheads < 1 || nheads > GGNN_MAX_HEADS)
     return fail(GGNN_EINVAL, std::string(what) + ": 1.." + std::to_string(GGNN_MAX_HEADS) + " heads");
   const size_t rows = (size_t)d->b * d->v, K = 2 * (size_t)d->h;
-  size_t o = 0;
+  int Ot = 0;
   for (int i = 0; i < nheads; ++i) {
     if (heads[i].o < 1 || heads[i].o > HEAD_MAXO || !heads[i].weight || !heads[i].bias)
       return fail(GGNN_EINVAL, std::string(what) + ": bad head " + std::to_string(i));
-    const size_t w = (size_t)heads[i].o;
-    L->Wd[i] = o; o += al(K * w * 4);
-    L->S[i] = o;  o += al(K * w * 4);
-    L->dZ[i] = o; o += al(rows * w * 4);
+    L->off[i] = Ot;
+    Ot += (heads[i].o + 3) & ~3;
   }
+  L->Ot = Ot;
+  size_t o = 0;
+  L->W = o;    o += al(K * Ot * 4);     // dropped weights W * mask / keep
+  L->Sx = o;   o += al(K * Ot * 4);     // mask / keep
+  L->bias = o; o += al((size_t)Ot * 4);
+  L->Z = o;    o += al(rows * Ot * 4);  // logits
+  L->dZ = o;   o += al(rows * Ot * 4);
+  L->dW = o;   o += al(K * Ot * 4);
+  L->lp = o;   o += al((size_t)nheads * HEAD_LP * 4);
   L->total = o;
   return GGNN_OK;
 }
@@ -1136,30 +1150,44 @@ int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nh
   if (int e = check_keep(keep, "heads_forward")) return e;
   if (!hT || !h0 || !ws) return fail(GGNN_EINVAL, "heads_forward: NULL pointer");
   if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_forward: target_num must be > 0");
+  for (int i = 0; i < nheads; ++i)
+    if (!heads[i].probs) return fail(GGNN_EINVAL, "heads_forward: NULL probs");
   hipStream_t s = (hipStream_t)stream;
-  const int H = d->h, K = 2 * H;
+  const int H = d->h, K = 2 * H, Ot = L.Ot;
   const long rows = (long)d->b * d->v;
   const Drop dr = make_drop(keep, seed);
-  if (loss) HIPCHK(hipMemsetAsync(loss, 0, (size_t)nheads * 4, s));
   Prof p(K_HEADS, s);
+  float* W = P<float>(ws, L.W);
+  float* Z = P<float>(ws, L.Z);
+  for (int i = 0; i < nheads; ++i) {
+    const int o = heads[i].o, op = (o + 3) & ~3;
+    hipLaunchKernelGGL(k_head_wdrop, dim3(grid1d((long)K * op)), dim3(256), 0, s, heads[i].weight, heads[i].bias, K, o,
+                       op, Ot, L.off[i], i, dr, W, P<float>(ws, L.Sx), P<float>(ws, L.bias));
+  }
+  // z = [hT | h0] W + b for every head at once, on MFMA (split f16 limbs, fp32
+  // accumulation): two terms, one per half of the concatenation
+  GemmArgs q = gg_args();
+  q.A = hT; q.A2 = h0; q.sAm = H; q.sAk = 1;
+  q.B = W; q.sBq = (long)H * Ot; q.sBk = Ot; q.sBn = 1;
+  q.D = Z; q.sDm = Ot; q.sDn = 1;
+  q.bias = P<const float>(ws, L.bias);
+  q.nterm = 2; q.M = (int)rows; q.N = Ot; q.K = H;
+  if (int e = gg_launch<PREC_SPLIT>(q, false, true, false, -1, s)) return e;
+  const unsigned nb = (unsigned)std::min<long>(HEAD_LP, (rows + 7) / 8);
   for (int i = 0; i < nheads; ++i) {
     const ggnn_output_head& hd = heads[i];
-    if (!hd.probs) return fail(GGNN_EINVAL, "heads_forward: NULL probs");
     const int o = hd.o;
-    float* Wd = P<float>(ws, L.Wd[i]);
-    float* S = P<float>(ws, L.S[i]);
-    hipLaunchKernelGGL(k_head_wdrop, dim3(grid1d((long)K * o)), dim3(256), 0, s, hd.weight, K, o, i, dr, Wd, S);
-    // z = [hT | h0] Wd + b on MFMA (split f16 limbs, fp32 accumulation): two
-    // terms, one per half of the concatenation
-    GemmArgs q = gg_args();
-    q.A = hT; q.A2 = h0; q.sAm = H; q.sAk = 1;
-    q.B = Wd; q.sBq = (long)H * o; q.sBk = o; q.sBn = 1;
-    q.D = hd.probs; q.sDm = o; q.sDn = 1;
-    q.bias = hd.bias;
-    q.nterm = 2; q.M = (int)rows; q.N = o; q.K = H;
-    if (int e = gg_launch<PREC_SPLIT>(q, false, true, false, -1, s)) return e;
-    hipLaunchKernelGGL(k_head_softmax, dim3((unsigned)std::min<long>(2048, (rows + 3) / 4)), dim3(256), 0, s, hd.probs,
-                       loss ? hd.labels : (const float*)nullptr, rows, o, 1.0f / target_num, loss ? loss + i : nullptr);
+    const float* y = loss ? hd.labels : (const float*)nullptr;
+    float* lp = P<float>(ws, L.lp) + (long)i * HEAD_LP;
+#define HSM(NI_)                                                                                                  \
+  hipLaunchKernelGGL(k_head_softmax<NI_>, dim3(nb), dim3(256), 0, s, Z + L.off[i], Ot, hd.probs, y, rows, o, \
+                     1.0f / target_num, lp)
+    if (o <= 64) HSM(1);
+    else if (o <= 128) HSM(2);
+    else if (o <= 256) HSM(4);
+    else HSM(HEAD_MAXO / 64);
+#undef HSM
+    if (loss) hipLaunchKernelGGL(k_head_loss, dim3(1), dim3(256), 0, s, lp, (int)nb, loss + i);
   }
   LAUNCHCHK();
   return GGNN_OK;
@@ -1173,56 +1201,64 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
   if (!hT || !h0 || !ws || !dhT || !dh0) return fail(GGNN_EINVAL, "heads_backward: NULL pointer");
   if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_backward: target_num must be > 0");
   hipStream_t s = (hipStream_t)stream;
-  const int H = d->h, K = 2 * H;
+  const int H = d->h, K = 2 * H, Ot = L.Ot;
   const long rows = (long)d->b * d->v;
   for (int i = 0; i < nheads; ++i)
     if (!heads[i].labels || !heads[i].probs || !heads[i].d_weight || !heads[i].d_bias)
       return fail(GGNN_EINVAL, "heads_backward: head needs labels, probs, d_weight, d_bias");
   Prof p(K_HEADS, s);
+  float* dZ = P<float>(ws, L.dZ);
+  float* dW = P<float>(ws, L.dW);
   {
     Zeroer z(s);
-    for (int i = 0; i < nheads; ++i) {
-      z.add(heads[i].d_weight, (long)K * heads[i].o);
-      z.add(heads[i].d_bias, heads[i].o);
-    }
+    for (int i = 0; i < nheads; ++i) z.add(heads[i].d_bias, heads[i].o);
+    z.add(dW, (long)K * Ot);
   }
   for (int i = 0; i < nheads; ++i) {
     const ggnn_output_head& hd = heads[i];
-    const int o = hd.o;
-    float* dZ = P<float>(ws, L.dZ[i]);
-    hipLaunchKernelGGL(k_head_dz, dim3((unsigned)std::min<long>(512, (rows + 3) / 4)), dim3(256), 0, s, hd.probs,
-                       hd.labels, rows, o, 1.0f / target_num, d_loss, dZ, hd.d_bias);
-    // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
-    // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
-    int ex = 0;
-    frexpf(target_num, &ex);
-    const float S = ldexpf(1.0f, std::max(-100, std::min(100, ex - 1)));
-    const float* Wd = P<const float>(ws, L.Wd[i]);
-    // (hidden a multiple of 64: each product in one launch with the output /
-    // operand split at H; otherwise one launch per half)
-    const bool one = H % 64 == 0;
-    for (int half = 0; half < (one ? 1 : 2); ++half) {
-      // [dhT | dh0] (+)= dZ Wd^T  (B(k=j, n=c) = Wd[c][j])
-      GemmArgs q = gg_args();
-      q.A = dZ; q.sAm = o; q.sAk = 1; q.scA = S; q.alpha = 1.0f / S;
-      q.B = Wd + (long)half * H * o; q.sBk = 1; q.sBn = o;
-      q.D = half ? dh0 : dhT; q.sDm = H; q.sDn = 1; q.mode = i > 0 ? GG_ADD : GG_STORE;
-      q.M = (int)rows; q.N = one ? 2 * H : H; q.K = o;
-      if (one) { q.D2 = dh0; q.Nsplit = H; }
-      if (int e = gg_launch<PREC_SPLIT>(q, false, true, true, -1, s)) return e;
-      // dW[rows of the half] += S_drop * ([hT | h0]^T dZ): split-K over node rows, atomics
-      const long KC = std::max<long>(256, ((rows + 47) / 48 + 31) & ~31L);
-      GemmArgs w = gg_args();
-      w.A = half ? h0 : hT; w.sAp = KC * H; w.sAm = 1; w.sAk = H;
-      w.B = dZ; w.sBp = KC * o; w.sBk = o; w.sBn = 1; w.scB = S; w.alpha = 1.0f / S;
-      w.D = hd.d_weight + (long)half * H * o; w.sDm = o; w.sDn = 1; w.mode = GG_ATOMIC;
-      w.E = P<const float>(ws, L.S[i]) + (long)half * H * o;
-      w.Z = (int)((rows + KC - 1) / KC); w.M = one ? 2 * H : H; w.N = o; w.K = (int)KC; w.Ktot = rows; w.sKp = KC;
-      if (one) { w.Am2 = h0; w.Msplit = H; }
-      if (int e = gg_launch<PREC_SPLIT>(w, false, false, false, -1, s)) return e;
-    }
-
+    const int o = hd.o, op = (o + 3) & ~3;
+    const dim3 g((unsigned)std::min<long>(512, (rows + 7) / 8));
+#define HDZ(NI_)                                                                                                  \
+  hipLaunchKernelGGL(k_head_dz<NI_>, g, dim3(256), 0, s, hd.probs, hd.labels, rows, o, op, 1.0f / target_num, d_loss, \
+                     dZ + L.off[i], Ot, hd.d_bias)
+    if (op <= 64) HDZ(1);
+    else if (op <= 128) HDZ(2);
+    else if (op <= 256) HDZ(4);
+    else HDZ(HEAD_MAXO / 64);
+#undef HDZ
   }
+  // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
+  // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
+  int ex = 0;
+  frexpf(target_num, &ex);
+  const float S = ldexpf(1.0f, std::max(-100, std::min(100, ex - 1)));
+  const float* W = P<const float>(ws, L.W);
+  // (hidden a multiple of 64: each product in one launch with the output /
+  // operand split at H; otherwise one launch per half)
+  const bool one = H % 64 == 0;
+  const long KC = std::max<long>(256, ((rows + 47) / 48 + 31) & ~31L);
+  for (int half = 0; half < (one ? 1 : 2); ++half) {
+    // [dhT | dh0] = dZ W^T  (B(k=j, n=c) = W[c][j]; K = Ot: padding columns are zeros)
+    GemmArgs q = gg_args();
+    q.A = dZ; q.sAm = Ot; q.sAk = 1; q.scA = S; q.alpha = 1.0f / S;
+    q.B = W + (long)half * H * Ot; q.sBk = 1; q.sBn = Ot;
+    q.D = half ? dh0 : dhT; q.sDm = H; q.sDn = 1;
+    q.M = (int)rows; q.N = one ? 2 * H : H; q.K = Ot;
+    if (one) { q.D2 = dh0; q.Nsplit = H; }
+    if (int e = gg_launch<PREC_SPLIT>(q, false, true, true, -1, s)) return e;
+    // dW[rows of the half] += (mask / keep) * ([hT | h0]^T dZ): split-K over node rows, atomics
+    GemmArgs w = gg_args();
+    w.A = half ? h0 : hT; w.sAp = KC * H; w.sAm = 1; w.sAk = H;
+    w.B = dZ; w.sBp = KC * Ot; w.sBk = Ot; w.sBn = 1; w.scB = S; w.alpha = 1.0f / S;
+    w.D = dW + (long)half * H * Ot; w.sDm = Ot; w.sDn = 1; w.mode = GG_ATOMIC;
+    w.E = P<const float>(ws, L.Sx) + (long)half * H * Ot;
+    w.Z = (int)((rows + KC - 1) / KC); w.M = one ? 2 * H : H; w.N = Ot; w.K = (int)KC; w.Ktot = rows; w.sKp = KC;
+    if (one) { w.Am2 = h0; w.Msplit = H; }
+    if (int e = gg_launch<PREC_SPLIT>(w, false, false, false, -1, s)) return e;
+  }
+  for (int i = 0; i < nheads; ++i)
+    hipLaunchKernelGGL(k_head_dw_out, dim3(grid1d((long)K * heads[i].o)), dim3(256), 0, s, dW + L.off[i], Ot, K,
+                       heads[i].o, heads[i].d_weight);
   LAUNCHCHK();
   return GGNN_OK;
 }

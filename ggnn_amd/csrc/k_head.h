@@ -7,8 +7,10 @@
 //              chem_tensorflow.py:349-403:
 //                z = [h_T | h0] @ dropout(W) + b ;  p = softmax(z) over o
 //                loss = sum_rows -sum_o y log p / task_target_num
-// Small next to the propagation (b*v*2h*o MACs per head), so plain fp32 FMA
-// tiles (fp32 parity by construction) rather than MFMA limb products.
+// The three products of a head (logits, d[hT | h0], dW) run on the general
+// path's MFMA GEMM (k_gemm_ring / k_gemm, split f16 limbs in the fp32 mode);
+// this file holds the element-wise parts.  Wd and dZ rows are padded to a
+// multiple of 4 columns (zeros) so their 16-byte chunks stay whole.
 #pragma once
 #include "ggnn_common.h"
 
@@ -107,125 +109,94 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
 DEV uint4 head_words(const Drop& d, int hd, int i, int j) {
   return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)hd, 0xA0000000u), d.k0, d.k1);
 }
-// Wd = W * mask / keep and S = mask / keep ([K][o], K = 2H), once per step
-__global__ void k_head_wdrop(const float* __restrict__ W, int K, int o, int hd, Drop dr, float* __restrict__ Wd,
-                             float* __restrict__ S) {
-  const long total = (long)K * o;
+// head hd's columns [off, off + op) of the concatenated W * mask / keep and
+// mask / keep ([K][Ot], K = 2H; op = o rounded up to 4, padding zeros) and of
+// the concatenated bias, once per step
+__global__ void k_head_wdrop(const float* __restrict__ W, const float* __restrict__ bias, int K, int o, int op, int Ot,
+                             int off, int hd, Drop dr, float* __restrict__ Wd, float* __restrict__ S,
+                             float* __restrict__ ball) {
+  const long total = (long)K * op;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int i = (int)(e / o), j = (int)(e % o);
+    const int i = (int)(e / op), j = (int)(e % op);
+    const long d = (long)i * Ot + off + j;
+    if (i == 0) ball[off + j] = j < o ? bias[j] : 0.f;
+    if (j >= o) {
+      Wd[d] = 0.f;
+      S[d] = 0.f;
+      continue;
+    }
     const float s = dr.thr ? drop_apply(dr, u4_get(head_words(dr, hd, i, j), i & 3), 1.0f) : 1.0f;
-    S[e] = s;
-    Wd[e] = W[e] * s;
+    S[d] = s;
+    Wd[d] = W[(long)i * o + j] * s;
   }
 }
-
-// fp32 tile GEMM C[M][N] = sum_k A(m,k) B(k,n) over a K range (split-K over
-// blockIdx.z); 64x64 tiles, 256 threads, 4x4 outputs per thread.  The problem
-// type P supplies the operand reads (with the coalesced index fastest) and the
-// epilogue.
-template <class P>
-__global__ void __launch_bounds__(256) k_sgemm(P p) {
-  constexpr int BM = 64, BN = 64, BK = 16;
-  __shared__ float As[BK][BM + 4], Bs[BK][BN + 4];
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const long kper = (p.K + gridDim.z - 1) / gridDim.z;
-  const long kb = (long)blockIdx.z * kper, ke = min((long)p.K, kb + kper);
-  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  float acc[4][4] = {};
-  for (long k0 = kb; k0 < ke; k0 += BK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      int m, kk;
-      if (P::kAmFast) { m = e % BM; kk = e / BM; } else { kk = e % BK; m = e / BK; }
-      const long k = k0 + kk;
-      As[kk][m] = (m0 + m < p.M && k < ke) ? p.a(m0 + m, k) : 0.f;
-      int n, kk2;
-      if (P::kBnFast) { n = e % BN; kk2 = e / BN; } else { kk2 = e % BK; n = e / BK; }
-      const long k2 = k0 + kk2;
-      Bs[kk2][n] = (n0 + n < p.N && k2 < ke) ? p.b(k2, n0 + n) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < BK; ++kk) {
-      float av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = As[kk][ty + 16 * i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tx + 16 * j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
-      if (m < p.M && n < p.N) p.store(m, n, acc[i][j]);
-    }
+// d_weight [K][o] = head's columns of the concatenated dW [K][Ot]
+__global__ void k_head_dw_out(const float* __restrict__ dWall, int Ot, int K, int o, float* __restrict__ dW) {
+  const long total = (long)K * o;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x)
+    dW[e] = dWall[(e / o) * Ot + e % o];
+}
+// loss = sum of the softmax blocks' partials (one block)
+__global__ void __launch_bounds__(256) k_head_loss(const float* __restrict__ lp, int n, float* __restrict__ loss) {
+  float x = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) x += lp[i];
+  for (int s = 32; s >= 1; s >>= 1) x += __shfl_xor(x, s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) *loss = red[0] + red[1] + red[2] + red[3];
 }
 
-// z[r][j] = [hT | h0][r] . Wd[:, j] + b[j]
-struct HeadLogitsP {
-  static constexpr bool kAmFast = false, kBnFast = true;
-  const float *hT, *h0, *Wd, *bias;
-  float* z;
-  int M, N, K, H;
-  DEV float a(int m, long k) const { return k < H ? hT[(long)m * H + k] : h0[(long)m * H + (k - H)]; }
-  DEV float b(long k, int n) const { return Wd[k * N + n]; }
-  DEV void store(int m, int n, float v) const { z[(long)m * N + n] = v + bias[n]; }
-};
-// [dhT | dh0][r][c] (+)= sum_j dZ[r][j] Wd[c][j]
-struct HeadDxP {
-  static constexpr bool kAmFast = false, kBnFast = false;
-  const float *dZ, *Wd;
-  float *dhT, *dh0;
-  int M, N, K, H, accumulate;
-  DEV float a(int m, long k) const { return dZ[(long)m * K + k]; }
-  DEV float b(long k, int n) const { return Wd[(long)n * K + k]; }
-  DEV void store(int m, int n, float v) const {
-    float* d = n < H ? dhT + (long)m * H + n : dh0 + (long)m * H + (n - H);
-    *d = accumulate ? *d + v : v;
-  }
-};
-// dW[c][j] += S[c][j] * sum_r [hT | h0][r][c] dZ[r][j]   (split over rows: atomics)
-struct HeadDwP {
-  static constexpr bool kAmFast = true, kBnFast = true;
-  const float *hT, *h0, *dZ, *S;
-  float* dW;
-  int M, N, H;
-  long K;
-  DEV float a(int m, long k) const { return m < H ? hT[k * H + m] : h0[k * H + (m - H)]; }
-  DEV float b(long k, int n) const { return dZ[k * N + n]; }
-  DEV void store(int m, int n, float v) const { atomicAdd(dW + (long)m * N + n, v * S[(long)m * N + n]); }
-};
-
-// in place z -> p = softmax(z) per row (one wave per row, rows grid-strided
-// over a few hundred blocks), loss += -sum y log p / num (one atomic per block:
-// one per 4 rows serialised 8192 same-address atomics at b*v = 32768)
-__global__ void __launch_bounds__(256) k_head_softmax(float* __restrict__ zp, const float* __restrict__ y, long rows,
-                                                      int o, float inv_num, float* __restrict__ loss) {
+// p = softmax(z) per row (z: a head's columns of the concatenated logits, row
+// stride zs), and the block's share of -sum y log p / num (lpart[block],
+// summed by k_head_loss: same-address atomics from every block serialise).
+// One wave per row, two rows per iteration, rows held in registers (lane l:
+// columns l + 64 i, o <= HEAD_MAXO): one load round trip per row pair.
+#define HEAD_MAXO 1024
+template <int NI>
+__global__ void __launch_bounds__(256) k_head_softmax(const float* __restrict__ zin, int zs, float* __restrict__ pout,
+                                                      const float* __restrict__ y, long rows, int o, float inv_num,
+                                                      float* __restrict__ lpart) {
   const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * 4;
   float term = 0.f;
-  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) {
-    float* z = zp + r * o;
-    float mx = -INFINITY;
-    for (int j = lane; j < o; j += 64) mx = fmaxf(mx, z[j]);
-    for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
-    float se = 0.f;
-    for (int j = lane; j < o; j += 64) se += expf(z[j] - mx);
-    for (int s = 32; s >= 1; s >>= 1) se += __shfl_xor(se, s);
-    const float lse = mx + logf(se);
-    for (int j = lane; j < o; j += 64) {
-      const float zj = z[j];
-      // log p computed as z - logsumexp (the reference takes log(softmax): the
-      // same value wherever softmax does not underflow to 0)
-      if (y) term -= y[r * o + j] * (zj - lse);
-      z[j] = expf(zj - lse);
+  // two rows per wave and iteration: both rows' loads in flight together
+  for (long r0 = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r0 < rows; r0 += 2 * stride) {
+    float x[2][NI], yy[2][NI];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long r = r0 + u * stride;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = lane + 64 * i;
+        const bool ok = r < rows && j < o;
+        x[u][i] = ok ? zin[r * zs + j] : -INFINITY;
+        yy[u][i] = (y && ok) ? y[r * o + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long r = r0 + u * stride;
+      if (r >= rows) break;
+      float mx = x[u][0];
+#pragma unroll
+      for (int i = 1; i < NI; ++i) mx = fmaxf(mx, x[u][i]);
+      for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+      float se = 0.f;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) se += lane + 64 * i < o ? expf(x[u][i] - mx) : 0.f;
+      for (int s = 32; s >= 1; s >>= 1) se += __shfl_xor(se, s);
+      const float lse = mx + logf(se);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = lane + 64 * i;
+        if (j < o) {
+          // log p computed as z - logsumexp (the reference takes log(softmax): the
+          // same value wherever softmax does not underflow to 0)
+          term -= yy[u][i] * (x[u][i] - lse);
+          pout[r * o + j] = expf(x[u][i] - lse);
+        }
+      }
     }
   }
   if (y) {
@@ -233,7 +204,7 @@ __global__ void __launch_bounds__(256) k_head_softmax(float* __restrict__ zp, co
     __shared__ float red[4];
     if (lane == 0) red[threadIdx.x >> 6] = term;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(loss, (red[0] + red[1] + red[2] + red[3]) * inv_num);
+    if (threadIdx.x == 0) lpart[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * inv_num;
   }
 }
 
@@ -241,28 +212,50 @@ __global__ void __launch_bounds__(256) k_head_softmax(float* __restrict__ zp, co
 // the bias gradient db[j] += sum_r dZ[r][j]: column partials in registers
 // (lane l owns columns l + 64i, o <= HEAD_MAXO), summed over the block's waves
 // in LDS, one global atomic per column per block
-#define HEAD_MAXO 1024
+// (dZ: the head's columns of the concatenated [rows][ldz] array, padded to op
+// with zeros; the row's p and y held in registers)
+template <int NI>
 __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, const float* __restrict__ y, long rows,
-                                                 int o, float inv_num, const float* __restrict__ dloss,
-                                                 float* __restrict__ dZ, float* __restrict__ db) {
-  constexpr int NI = HEAD_MAXO / 64;
-  __shared__ float cs[4][HEAD_MAXO];
+                                                 int o, int op, float inv_num, const float* __restrict__ dloss,
+                                                 float* __restrict__ dZ, int ldz, float* __restrict__ db) {
+  __shared__ float cs[4][NI * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float g = (dloss ? *dloss : 1.0f) * inv_num;
   float part[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) part[i] = 0.f;
-  for (long r = (long)blockIdx.x * 4 + w; r < rows; r += (long)gridDim.x * 4) {
-    float sy = 0.f;
-    for (int j = lane; j < o; j += 64) sy += y[r * o + j];
-    for (int s = 32; s >= 1; s >>= 1) sy += __shfl_xor(sy, s);
+  const long stride = (long)gridDim.x * 4;
+  for (long r0 = (long)blockIdx.x * 4 + w; r0 < rows; r0 += 2 * stride) {
+    float pv[2][NI], yv[2][NI];
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int j = lane + 64 * i;
-      if (j < o) {
-        const float d = g * (p[r * o + j] * sy - y[r * o + j]);
-        dZ[r * o + j] = d;
-        part[i] += d;
+    for (int u = 0; u < 2; ++u) {
+      const long r = r0 + u * stride;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = lane + 64 * i;
+        const bool ok = r < rows && j < o;
+        pv[u][i] = ok ? p[r * o + j] : 0.f;
+        yv[u][i] = ok ? y[r * o + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long r = r0 + u * stride;
+      if (r >= rows) break;
+      float sy = 0.f;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) sy += yv[u][i];
+      for (int s = 32; s >= 1; s >>= 1) sy += __shfl_xor(sy, s);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = lane + 64 * i;
+        if (j < o) {
+          const float d = g * (pv[u][i] * sy - yv[u][i]);
+          dZ[r * ldz + j] = d;
+          part[i] += d;
+        } else if (j < op) {
+          dZ[r * ldz + j] = 0.f;
+        }
       }
     }
   }
@@ -271,13 +264,4 @@ __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, co
     if (lane + 64 * i < o) cs[w][lane + 64 * i] = part[i];
   __syncthreads();
   for (int j = threadIdx.x; j < o; j += 256) atomicAdd(db + j, cs[0][j] + cs[1][j] + cs[2][j] + cs[3][j]);
-}
-
-// db[j] = sum_r dZ[r][j] (2D grid: blockIdx.y strides the rows; atomics)
-__global__ void k_colsum(const float* __restrict__ dZ, long rows, int o, float* __restrict__ db) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= o) return;
-  float s = 0.f;
-  for (long r = blockIdx.y; r < rows; r += gridDim.y) s += dZ[r * o + j];
-  atomicAdd(db + j, s);
 }
