@@ -234,15 +234,17 @@ def callers_side(dev, b, v, h, reps=10):
                     "wide, heads o=150 and 46"}
 
 
-def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10):
+def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10, unfused=False):
     """The same fwd+bwd step in a reduced-precision mode (single 16-bit MFMA
     operands): graphs/s and the prop kernels' fraction of the dense bf16 MFMA
-    peak (north_star's >= 30 % target is quoted on bf16 tiles)."""
+    peak (north_star's >= 30 % target is quoted on bf16 tiles).  unfused: the
+    forward as separate k_prop_fwd + k_gru_fwd launches (GGNN_UNFUSED_FWD), the
+    kernels north_star's adj x h and fused-GRU targets name."""
     import torch
     from ggnn_amd import _lib
     from ggnn_amd.dist import FlatGradients
     from ggnn_amd.engine import PropagationEngine
-    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=precision)
+    eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=precision, unfused_forward=unfused)
     grads = FlatGradients(h, C, True, device=dev)
     gv = dict(grads.views)
     gv["h0"] = torch.empty((b, v, h), dtype=torch.float32, device=dev)
@@ -277,8 +279,16 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10)
                          frac_roofline=max(d["frac_of_bf16_peak"], gbs / HBM_PEAK_GBS),
                          traffic_source="profiles/pmc_traffic_%s.json" % precision)
             fr[k] = d
-    return {"precision": precision, "value": b / (ms * 1e-3), "unit": "graphs/s", "ms_per_step": ms,
-            "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
+    out = {"precision": precision, "value": b / (ms * 1e-3), "unit": "graphs/s", "ms_per_step": ms,
+           "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
+    if not unfused:
+        u = precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps, unfused=True)
+        out["unfused_forward"] = {"value": u["value"], "ms_per_step": u["ms_per_step"],
+                                  "kernels": {k: u["kernels"][k] for k in ("prop_fwd", "gru_fwd") if k in u["kernels"]},
+                                  "note": "the forward as per-timestep k_prop_fwd + k_gru_fwd launches "
+                                          "(GGNN_UNFUSED_FWD): north_star's adj x h (>= 30 % of bf16 MFMA peak) "
+                                          "and fused-GRU (>= 50 % of HBM peak) targets are quoted on these kernels"}
+    return out
 
 
 def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
@@ -409,6 +419,9 @@ def main():
     ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (default nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
+    ap.add_argument("--pmc-unfused-leg", action="store_true",
+                    help="after the timed work, two steps with the unfused forward (k_prop_fwd + k_gru_fwd), so a "
+                         "PMC pass over this command covers those kernels too (tools/profile_round.sh)")
     ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
                     help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
                          "parity mode); fp16 / bf16: single 16-bit MFMA operands (reduced precision)")
@@ -499,6 +512,16 @@ def main():
         tt = torch.tensor([dt, dt_drop], dtype=torch.float64, device=dev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         dt, dt_drop = float(tt[0].item()), float(tt[1].item())
+
+    if args.pmc_unfused_leg:
+        ueng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision,
+                                 unfused_forward=True)
+        for _ in range(2):
+            pack = ueng.pack_weights(w_d, T=T)
+            ueng.set_adjacency(A_d)
+            ueng.forward(h0_d, pack, T, training=True, out=out)
+            ueng.backward(dhT, gviews)
+        barrier()
 
     # roofline of the dominant kernel (largest total time in the timed region)
     kinds = {k: ms for k, ms in timer.total_ms.items() if timer.launches.get(k)}
