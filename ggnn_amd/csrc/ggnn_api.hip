@@ -332,7 +332,7 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
   do {                                                                               \
     constexpr bool sp_ = Prec<PREC>::split;                                          \
     constexpr int mx_ = sp_ ? kSplitRT<FN##_tag>::value : kMaxRT<FN##_tag, H>::value; \
-    const int rt_ = gru_rt(c, mx_);                                                  \
+    const int rt_ = std::min(gru_rt(c, mx_), rt_cap<FN##_tag>());                    \
     if (mx_ >= 4 && rt_ == 4) FN<H, mx_ >= 4 ? 4 : 2, PREC>(__VA_ARGS__);            \
     else if (rt_ == 2) FN<H, 2, PREC>(__VA_ARGS__);                                  \
     else FN<H, 1, PREC>(__VA_ARGS__);                                                \
@@ -348,6 +348,15 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
 // registers) live through both products and spills at RT = 4.
 struct launch_gru_fwd_tag {};
 struct launch_gru_bwd_tag {};
+// GGNN_GRU_BWD_RT caps the GRU backward's row tiles (experiment knob)
+template <typename TAG> int rt_cap() { return 4; }
+template <> int rt_cap<launch_gru_bwd_tag>() {
+  static const int v = [] {
+    const char* e = getenv("GGNN_GRU_BWD_RT");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
+  return v;
+}
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
 template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
@@ -1068,7 +1077,7 @@ int ggnn_embed_forward(const ggnn_dims* d, const ggnn_embed_segment* segs, int n
   if (!word_inputs || !h0) return fail(GGNN_EINVAL, "embed_forward: NULL pointer");
   hipStream_t s = (hipStream_t)stream;
   Prof p(K_HEADS, s);
-  hipLaunchKernelGGL(k_embed_fwd, dim3(grid1d(a.rows * a.H)), dim3(256), 0, s, a, word_inputs, h0);
+  hipLaunchKernelGGL(k_embed_fwd, dim3(grid1d((a.rows + 3) / 4 * a.H)), dim3(256), 0, s, a, word_inputs, h0);
   LAUNCHCHK();
   return GGNN_OK;
 }
@@ -1092,7 +1101,7 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
     for (int i = 0; i < nseg; ++i) z.add(segs[i].d_table, (long)segs[i].rows * segs[i].width);
     z.add(lookup_sqnorm, nseg);
   }
-  hipLaunchKernelGGL(k_embed_bwd, dim3(std::min(grid1d(a.rows * a.H), 4096)), dim3(256), 0, s, a, gd, word_inputs,
+  hipLaunchKernelGGL(k_embed_bwd, dim3(std::min(grid1d((a.rows + 3) / 4 * a.H), 4096)), dim3(256), 0, s, a, gd, word_inputs,
                      dh0, dh0_add, lookup_sqnorm);
   LAUNCHCHK();
   return GGNN_OK;

@@ -41,21 +41,29 @@ DEV int emb_find(const EmbArgs& a, int k) {
   return s;
 }
 
-// h0 [rows][H]: one thread per element (tiny: b*v*H)
+// h0 [rows][H]: one thread per (row quad, column): one Philox block serves
+// the quad's 4 rows (its 4 words are the 4 rows' masks)
 __global__ void __launch_bounds__(256) k_embed_fwd(EmbArgs a, const int* __restrict__ wi, float* __restrict__ h0) {
-  const long total = a.rows * a.H;
+  const long nq = (a.rows + 3) >> 2, total = nq * a.H;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long r = e / a.H;
+    const long q = e / a.H;
     const int k = (int)(e % a.H);
     const int s = emb_find(a, k);
-    float x = 0.f;
-    if (s >= 0) {
-      const EmbSeg& S = a.s[s];
-      const int id = wi[r * a.ncols + S.column];
-      if (id >= 0 && id < S.rows) x = S.table[(long)id * S.width + (k - S.offset)];
-      if (a.dr.thr) x = drop_apply(a.dr, u4_get(emb_words(a.dr, r, k), (int)(r & 3)), x);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (s >= 0 && a.dr.thr) w = emb_words(a.dr, q * 4, k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long r = q * 4 + i;
+      if (r >= a.rows) break;
+      float x = 0.f;
+      if (s >= 0) {
+        const EmbSeg& S = a.s[s];
+        const int id = wi[r * a.ncols + S.column];
+        if (id >= 0 && id < S.rows) x = S.table[(long)id * S.width + (k - S.offset)];
+        if (a.dr.thr) x = drop_apply(a.dr, u4_get(w, i), x);
+      }
+      h0[r * a.H + k] = x;
     }
-    h0[e] = x;
   }
 }
 
@@ -63,6 +71,7 @@ __global__ void __launch_bounds__(256) k_embed_fwd(EmbArgs a, const int* __restr
 // zeroed by the host), and the sum of squares of the per-lookup gradient rows
 // per segment: the norm tf.clip_by_norm takes of an embedding's IndexedSlices
 // gradient (its values, duplicates not merged) -- chem_tensorflow.py:498-503.
+// One thread per (row quad, column), as k_embed_fwd.
 struct EmbGrad {
   float* dtable[EMB_MAXSEG];
 };
@@ -72,21 +81,29 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
   float acc[EMB_MAXSEG];
 #pragma unroll
   for (int i = 0; i < EMB_MAXSEG; ++i) acc[i] = 0.f;
-  const long total = a.rows * a.H;
+  const long nq = (a.rows + 3) >> 2, total = nq * a.H;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long r = e / a.H;
+    const long q = e / a.H;
     const int k = (int)(e % a.H);
     const int s = emb_find(a, k);
     if (s < 0) continue;
     const EmbSeg& S = a.s[s];
-    float g = dh0[e] + (dh0_add ? dh0_add[e] : 0.f);
-    if (a.dr.thr) g = drop_apply(a.dr, u4_get(emb_words(a.dr, r, k), (int)(r & 3)), g);
-    const int id = wi[r * a.ncols + S.column];
-    if (id < 0 || id >= S.rows) continue;
-    atomicAdd(gd.dtable[s] + (long)id * S.width + (k - S.offset), g);
+    const uint4 w = a.dr.thr ? emb_words(a.dr, q * 4, k) : make_uint4(0u, 0u, 0u, 0u);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long r = q * 4 + i;
+      if (r >= a.rows) break;
+      float g = dh0[r * a.H + k] + (dh0_add ? dh0_add[r * a.H + k] : 0.f);
+      if (a.dr.thr) g = drop_apply(a.dr, u4_get(w, i), g);
+      const int id = wi[r * a.ncols + S.column];
+      if (id < 0 || id >= S.rows) continue;
+      atomicAdd(gd.dtable[s] + (long)id * S.width + (k - S.offset), g);
+      ss += g * g;
+    }
 #pragma unroll
     for (int i = 0; i < EMB_MAXSEG; ++i)
-      if (i == s) acc[i] += g * g;
+      if (i == s) acc[i] += ss;
   }
   __shared__ float red[4][EMB_MAXSEG];
 #pragma unroll

@@ -26,22 +26,20 @@ def adj_mat_to_target(adj_mat, is_probability=False, true_target=None):
     (0/1 input) holds no exact 1, is skipped.  The first maximum in (edge type,
     source) row-major order wins, as ``np.where(...)[..][0]`` does there.
     ``true_target`` is accepted for signature parity (only used by a disabled
-    diagnostic in the reference)."""
+    diagnostic in the reference).  Vectorised over the nodes (the per-node loop
+    took half of run_epoch's host time at batch 20)."""
     a = np.asarray(adj_mat)
     num_e, num_v, num_o = a.shape
-    graph = []
-    for node in range(1, num_v):
-        sl = a[:, node, :]
-        mx = np.amax(sl)
-        if mx == 0:
-            continue
-        flat = sl.reshape(-1)
-        hits = np.flatnonzero(flat == (mx if is_probability else 1))
-        if hits.size == 0:
-            continue
-        e, src = divmod(int(hits[0]), num_o)
-        graph.append([src, e + 1])
-    return graph
+    if num_v < 2:
+        return []
+    # row n-1 = node n's [e, o] slice flattened in (edge type, source) order
+    t = np.transpose(a[:, 1:, :], (1, 0, 2)).reshape(num_v - 1, num_e * num_o)
+    mx = t.max(axis=1)
+    eq = t == (mx[:, None] if is_probability else 1)
+    keep = (mx != 0) & eq.any(axis=1)  # (a NaN maximum matches nothing: skipped)
+    first = eq.argmax(axis=1)
+    e, src = np.divmod(first[keep], num_o)
+    return [[int(x), int(y) + 1] for x, y in zip(src, e)]
 
 
 def get_las_uas(target_graph, result_graph, is_edge=False):

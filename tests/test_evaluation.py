@@ -147,3 +147,44 @@ def test_adam_step_count_survives_float32_underflow():
         assert _adam_step_count({"weights": w}, opt) == t, t
         assert _adam_step_count({"weights": w, "adam_step": t}, opt) == t
     assert _adam_step_count({"weights": {}}, opt) is None
+
+
+def _adj_mat_to_target_loop(adj_mat, is_probability=False):
+    """The per-node loop of chem_tensorflow_dense.py:106-131, restated as is."""
+    a = np.asarray(adj_mat)
+    ne, nv, no = a.shape
+    g = []
+    for node in range(1, nv):
+        sl = a[:, node, :]
+        mx = np.amax(sl)
+        if mx == 0:
+            continue
+        hits = np.flatnonzero(sl.reshape(-1) == (mx if is_probability else 1))
+        if hits.size == 0:
+            continue
+        e, src = divmod(int(hits[0]), no)
+        g.append([src, e + 1])
+    return g
+
+
+def test_adj_mat_to_target_vectorised_matches_loop():
+    """The vectorised adj_mat_to_target against the reference's per-node loop:
+    0/1 targets, probabilities with ties and zeros, negatives, NaN rows."""
+    from ggnn_amd import evaluation as E
+    rng = np.random.default_rng(0)
+    for trial in range(600):
+        ne, nv, no = int(rng.integers(1, 5)), int(rng.integers(1, 12)), int(rng.integers(1, 12))
+        kind = trial % 4
+        if kind == 0:
+            a = (rng.random((ne, nv, no)) < 0.1).astype(np.float32)
+        elif kind == 1:
+            a = (rng.random((ne, nv, no)) * (rng.random((ne, nv, no)) < 0.5)).astype(np.float32)
+        elif kind == 2:
+            a = rng.integers(0, 3, (ne, nv, no)).astype(np.float32)
+            a[rng.random(a.shape) < 0.05] = -1
+        else:
+            a = np.round(rng.random((ne, nv, no)), 1).astype(np.float32)
+        if trial % 50 == 0:
+            a[0, min(1, nv - 1), 0] = np.nan
+        for p in (False, True):
+            assert E.adj_mat_to_target(a, p) == _adj_mat_to_target_loop(a, p), (trial, p)
