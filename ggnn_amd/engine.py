@@ -13,6 +13,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
+from .upload import Uploader
 
 WEIGHT_NAMES = ("edge_weights", "edge_biases", "gates_kernel", "gates_bias",
                 "candidate_kernel", "candidate_bias")
@@ -74,6 +75,7 @@ class PropagationEngine:
         self.h = int(hidden)
         self.C = int(channels)
         self.use_edge_bias = bool(use_edge_bias)
+        self._up_edges, self._up_offs = Uploader(), Uploader()
         if precision not in _lib.PRECISIONS:
             raise ValueError("precision must be one of %s" % (_lib.PRECISIONS,))
         self.precision = precision
@@ -182,8 +184,8 @@ class PropagationEngine:
                     raise IndexError("edge label outside 1..%d" % E)
                 if min(src.min(), dst.min()) < 0 or max(src.max(), dst.max()) >= v:
                     raise IndexError("edge node index outside 0..%d" % (v - 1))
-            edges = torch.from_numpy(np.ascontiguousarray(e_np)).to(self.device)
-            offs = torch.from_numpy(offs_np).to(self.device)
+            edges = self._up_edges(e_np, self.device)
+            offs = self._up_offs(offs_np, self.device)
         d = self.dims(b, v, 1)
         nbytes = _lib.adjacency_bytes(d)
         if self._adj is None or self._adj.numel() < nbytes:

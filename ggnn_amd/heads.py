@@ -19,6 +19,8 @@ import ctypes
 import numpy as np
 import torch
 
+from .upload import Uploader
+
 from . import _lib
 
 SMALL_NUMBER = 1e-7   # utils.py
@@ -49,6 +51,9 @@ def _f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
+_WI_UPLOAD = Uploader()
+
+
 def word_inputs_tensor(word_inputs, device, table_rows=None) -> torch.Tensor:
     """The feed's ``word_inputs`` [b, v, ncols] (float64 in the reference's feed)
     as int32 on the device.  ``table_rows``: {column: rows} to validate (the
@@ -61,7 +66,7 @@ def word_inputs_tensor(word_inputs, device, table_rows=None) -> torch.Tensor:
             if c.size and (c.min() < 0 or c.max() >= rows):
                 raise IndexError("word_inputs[..., %d] holds index %d outside [0, %d)"
                                  % (col, int(c.max() if c.max() >= rows else c.min()), rows))
-    return torch.from_numpy(np.ascontiguousarray(wi_i.astype(np.int32))).to(device)
+    return _WI_UPLOAD(wi_i.astype(np.int32), device)
 
 
 class EmbeddingFrontEnd:

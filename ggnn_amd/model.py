@@ -41,6 +41,7 @@ from .batching import BtbBatching, ThreadedIterator
 from .engine import PropagationEngine
 from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
 from .optim import ClipAdam
+from .upload import Uploader
 
 GRU_KEYS = ("gates_kernel", "gates_bias", "candidate_kernel", "candidate_bias")
 
@@ -123,6 +124,7 @@ class DenseGGNNChemModel(BtbBatching):
         self.weights = {}
         self.ops = {}
         self._engines = {}
+        self._up_labels, self._up_labels_e = Uploader(), Uploader()
         rs = self.params["random_seed"] if seed is None else seed
         self._rng = np.random.RandomState(rs)
         self.prepare_specific_graph_model()
@@ -320,9 +322,11 @@ class DenseGGNNChemModel(BtbBatching):
         o, oe = self.params["output_size"], self.output_size_edges
         if v > o:
             raise ValueError("num_vertices %d > output_size %d" % (v, o))
-        y_h = torch.from_numpy(np.asarray(self.placeholders["target_values_head"], np.float32).reshape(b, v, o))
-        y_e = torch.from_numpy(np.asarray(self.placeholders["target_values_edges"], np.float32).reshape(b, v, oe))
-        labels = [y_h.to(self.device), y_e.to(self.device)]
+        y_h = self._up_labels(np.asarray(self.placeholders["target_values_head"], np.float32).reshape(b, v, o),
+                              self.device)
+        y_e = self._up_labels_e(np.asarray(self.placeholders["target_values_edges"], np.float32).reshape(b, v, oe),
+                                self.device)
+        labels = [y_h, y_e]
         tmask = np.asarray(self.placeholders["target_mask"], np.float64)
         internal = self.params["task_ids"].index(task_id)
         target_num = float(tmask[internal].sum() + SMALL_NUMBER)
