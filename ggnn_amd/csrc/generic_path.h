@@ -336,10 +336,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   for (int t = c.T - 1; t >= 0; --t) {
     const float* ht = P<float>(ws, L.hsl(t));
     const float* G = P<float>(ws, L.g(t));
+    // (row slices of the element-wise kernels: ~256 rows each, one bias atomic per column per slice)
+    const dim3 ewg((unsigned)((H + 255) / 256), (unsigned)std::max<long>(1, std::min<long>(512, N / 64)));
     {
       Prof p(K_GRU_BWD, s);
-      hipLaunchKernelGGL(k_gen_bwd1, dim3(grid1d(N * H)), dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)),
-                         DZC, DZG, DXH, N, c.H);
+      hipLaunchKernelGGL(k_gen_bwd1, ewg, dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)), DZC, DZG, DXH, N,
+                         c.H, dbc, dbg);
     }
     // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k])
     for (int half = 0; half < 2; ++half) {
@@ -352,7 +354,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     }
     {
       Prof p(K_GRU_BWD, s);
-      hipLaunchKernelGGL(k_gen_bwd2, dim3(grid1d(N * H)), dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H);
+      hipLaunchKernelGGL(k_gen_bwd2, ewg, dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H, dbg);
     }
     // [dX | dh] += dzg Wg^T
     {
@@ -376,13 +378,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     if (int e = wg(P<float>(ws, L.rh(t)), DZC, H, (int)H, dWc + H * H, H)) return e;
     if (int e = wg(P<float>(ws, L.x(t)), DZG, 2 * H, (int)(2 * H), dWg, 2 * H)) return e;
     if (int e = wg(ht, DZG, 2 * H, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
-    {
-      Prof p(K_WGRAD, s);
-      const unsigned ys = (unsigned)std::max<long>(1, std::min<long>(256, N / 64));
-      hipLaunchKernelGGL(k_gen_colsum, dim3((unsigned)((H + 255) / 256), ys), dim3(256), 0, s, DZC, N, c.H, H, dbc);
-      hipLaunchKernelGGL(k_gen_colsum, dim3((unsigned)((2 * H + 255) / 256), ys), dim3(256), 0, s, DZG, N,
-                         (int)(2 * H), 2 * H, dbg);
-    }
     // dM[g,c] = A[g,c]^T dX[g] over the non-empty tiles
     {
       GemmArgs a = gg_args();
@@ -391,6 +386,8 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.D = dM; a.sDz = v * H; a.sDm = H; a.sDn = 1;
       a.zdiv = (int)C; a.Z = (int)(c.b * C); a.zmask = dense_ch ? nullptr : P<unsigned char>(adj, AL.occ);
       a.M = (int)v; a.N = (int)H; a.K = (int)v;
+      // dbeta_c += column sums of dM[g,c] (the edge bias enters every message row)
+      if (use_bias) { a.csum = dbeta; a.scq = H; }
       if (int e = gg_launch<PREC>(a, true, true, false, K_PROP_BWD, s)) return e;
     }
     // dh[g] += sum over g's channels of dM[g,c] W_c^T
@@ -403,7 +400,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.Z = c.b; a.M = (int)v; a.N = (int)H; a.K = (int)H;
       if (int e = gg_launch<PREC>(a, false, true, true, K_PROP_BWD, s)) return e;
     }
-    // dW_c (+)= sum over c's graphs of h_t[g]^T dM[g,c]; dbeta_c += column sums of dM[g,c]
+    // dW_c (+)= sum over c's graphs of h_t[g]^T dM[g,c]
     {
       float* G_out = c.ed ? P<float>(ws, L.GW) : dW;
       const bool chunked = AL.nch > 1;
@@ -420,9 +417,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       if (c.ed)
         hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * H * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
                            c.C, c.H, t, c.edrop);
-      if (use_bias)
-        hipLaunchKernelGGL(k_gen_dbeta, dim3((unsigned)((H + 63) / 64), (unsigned)C, (unsigned)std::min(c.b, 64)),
-                           dim3(256), 0, s, dM, P<const int>(adj, AL.cgl), c.b, c.C, c.vin, c.H, dbeta);
     }
     // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
     {

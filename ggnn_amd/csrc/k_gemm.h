@@ -61,6 +61,11 @@ struct GemmArgs {
   int Msplit;
   float* D2;
   int Nsplit;
+  // if set: csum[zp*scp + zq*scq + n] += sum over m of the stored values of
+  // column n (e.g. the edge-bias gradient from dM), one atomic per column per
+  // wave pair
+  float* csum;
+  long scp, scq;
 };
 
 namespace gg {
@@ -288,25 +293,32 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       const int n = n0 + wn * 32 * WN + 32 * j + l32;
-      if (n >= a.N) continue;
-      const float bn = bias ? bias[n] : 0.f;
-      const bool hi_n = a.Nsplit && n >= a.Nsplit;
+      float cs = 0.f;
+      if (n < a.N) {
+        const float bn = bias ? bias[n] : 0.f;
+        const bool hi_n = a.Nsplit && n >= a.Nsplit;
 #pragma unroll
-      for (int i = 0; i < WM; ++i)
+        for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
-          if (m >= a.M) continue;
-          float x = a.alpha * acc[i][j][r] + bn;
-          if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
-          else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-          const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
-          if (a.E) x *= a.E[doff];
-          float* d = (hi_n ? a.D2 : a.D) + doff;
-          if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-          else if (a.mode == GG_ADD) *d += x;
-          else *d = x;
-        }
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
+            if (m >= a.M) continue;
+            float x = a.alpha * acc[i][j][r] + bn;
+            if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
+            else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+            const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+            if (a.E) x *= a.E[doff];
+            cs += x;
+            float* d = (hi_n ? a.D2 : a.D) + doff;
+            if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+            else if (a.mode == GG_ADD) *d += x;
+            else *d = x;
+          }
+      }
+      if (a.csum) {
+        cs += __shfl_xor(cs, 32);
+        if (hh == 0 && n < a.N) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+      }
     }
     __syncthreads();  // the next z's prologue rewrites buffer 0
   }

@@ -270,24 +270,32 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + 32 * j + l32;
-    if (n >= a.N) continue;
-    const float bn = bias ? bias[n] : 0.f;
-    const bool hi_n = a.Nsplit && n >= a.Nsplit;
+    float cs = 0.f;
+    if (n < a.N) {
+      const float bn = bias ? bias[n] : 0.f;
+      const bool hi_n = a.Nsplit && n >= a.Nsplit;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + 32 * i + acc_row(r, hh);
-        if (m >= a.M) continue;
-        float x = a.alpha * acc[i][j][r] + bn;
-        if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
-        else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-        const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
-        if (a.E) x *= a.E[doff];
-        float* d = (hi_n ? a.D2 : a.D) + doff;
-        if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-        else if (a.mode == GG_ADD) *d += x;
-        else *d = x;
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + 32 * i + acc_row(r, hh);
+          if (m >= a.M) continue;
+          float x = a.alpha * acc[i][j][r] + bn;
+          if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
+          else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+          const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+          if (a.E) x *= a.E[doff];
+          cs += x;
+          float* d = (hi_n ? a.D2 : a.D) + doff;
+          if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+          else if (a.mode == GG_ADD) *d += x;
+          else *d = x;
+        }
+    }
+    // column sums (GemmArgs::csum): lanes l and l + 32 hold the same column
+    if (a.csum) {
+      cs += __shfl_xor(cs, 32);
+      if (hh == 0 && n < a.N) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+    }
   }
 }

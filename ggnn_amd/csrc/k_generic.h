@@ -139,30 +139,50 @@ __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict
 // ---- backward element-wise steps, timestep t (Appendix A of SURVEY.md):
 // e1: dc = d(1-u); du = d(h-c); dzc = dc(1-c^2); dzg_u = du u(1-u);
 //     dh (second half of the [N][2H] buffer DXH) = d u
-__global__ void k_gen_bwd1(const float* __restrict__ d, const float* __restrict__ G, const float* __restrict__ h,
-                           const float* __restrict__ cc, float* __restrict__ dzc, float* __restrict__ dzg,
-                           float* __restrict__ DXH, long N, int H) {
-  const long total = N * H;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long row = e / H;
-    const int k = (int)(e % H);
-    const float u = G[row * 2 * H + H + k], c = cc[e], dl = d[e];
-    dzc[e] = dl * (1.0f - u) * (1.0f - c * c);
-    dzg[row * 2 * H + H + k] = dl * (h[e] - c) * u * (1.0f - u);
-    DXH[row * 2 * H + H + k] = dl * u;
+__global__ void __launch_bounds__(256) k_gen_bwd1(const float* __restrict__ d, const float* __restrict__ G,
+                                                  const float* __restrict__ h, const float* __restrict__ cc,
+                                                  float* __restrict__ dzc, float* __restrict__ dzg,
+                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ dbc,
+                                                  float* __restrict__ dbg) {
+  // grid (column blocks, row slices): column k per thread, the slice's rows in
+  // turn; the bias gradients dbc = sum dzc, dbg[H:] = sum dzg_u as one atomic
+  // per column per block (no separate column-sum pass over dzc / dzg)
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H) return;
+  const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
+  float sc = 0.f, su = 0.f;
+  for (long row = r0; row < r1; ++row) {
+    const long e = row * H + k, g2 = row * 2 * H + H + k;
+    const float u = G[g2], c = cc[e], dl = d[e];
+    const float zc = dl * (1.0f - u) * (1.0f - c * c), zu = dl * (h[e] - c) * u * (1.0f - u);
+    dzc[e] = zc;
+    dzg[g2] = zu;
+    DXH[g2] = dl * u;
+    sc += zc;
+    su += zu;
+  }
+  if (r1 > r0) {
+    atomicAdd(dbc + k, sc);
+    atomicAdd(dbg + H + k, su);
   }
 }
-// e2: d(rh) -> dr = d(rh) h, dzg_r = dr r(1-r); dh += d(rh) r
-__global__ void k_gen_bwd2(const float* __restrict__ drh, const float* __restrict__ G, const float* __restrict__ h,
-                           float* __restrict__ dzg, float* __restrict__ DXH, long N, int H) {
-  const long total = N * H;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long row = e / H;
-    const int k = (int)(e % H);
+// e2: d(rh) -> dr = d(rh) h, dzg_r = dr r(1-r); dh += d(rh) r; dbg[:H] += sum dzg_r
+__global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh, const float* __restrict__ G,
+                                                  const float* __restrict__ h, float* __restrict__ dzg,
+                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ dbg) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H) return;
+  const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
+  float sr = 0.f;
+  for (long row = r0; row < r1; ++row) {
+    const long e = row * H + k;
     const float r = G[row * 2 * H + k], x = drh[e];
-    dzg[row * 2 * H + k] = x * h[e] * r * (1.0f - r);
+    const float zr = x * h[e] * r * (1.0f - r);
+    dzg[row * 2 * H + k] = zr;
     DXH[row * 2 * H + H + k] += x * r;
+    sr += zr;
   }
+  if (r1 > r0) atomicAdd(dbg + k, sr);
 }
 // dL/dh_t (second half of DXH) -> the next (earlier) step's delta: the state
 // dropout backward of timestep tm = t-1 (tm < 0: none), times osc (the
@@ -197,38 +217,4 @@ __global__ void k_gen_delta0(const float* __restrict__ dhT, float* __restrict__ 
     }
     out[e] = x;
   }
-}
-
-// column sums: out[n] += sum_rows X[row][n] (ld columns), rows split over
-// blockIdx.y with atomics
-__global__ void k_gen_colsum(const float* __restrict__ X, long rows, int ncol, long ld, float* __restrict__ out) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= ncol) return;
-  const long per = (rows + gridDim.y - 1) / gridDim.y;
-  const long r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
-  float s = 0.f;
-  for (long r = r0; r < r1; ++r) s += X[r * ld + n];
-  if (r1 > r0) atomicAdd(out + n, s);
-}
-// dbeta[c][n] += sum over the graphs g of channel c and nodes j of dM[g][c][j][n]:
-// grid (column blocks of 64, C, graph slices); 4 row groups per block summed in
-// LDS, one atomic per column per block
-__global__ void __launch_bounds__(256) k_gen_dbeta(const float* __restrict__ dM, const int* __restrict__ cgl, int b,
-                                                   int C, int v, int H, float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.y, n = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  const int* L = cgl + (long)c * (b + 1);
-  const int ng = L[0];
-  const int per = (ng + gridDim.z - 1) / gridDim.z;
-  const int e0 = blockIdx.z * per, e1 = min(ng, e0 + per);
-  float s = 0.f;
-  if (n < H)
-    for (int e = e0; e < e1; ++e) {
-      const float* p = dM + ((long)L[1 + e] * C + c) * v * H + n;
-      for (int j = rg; j < v; j += 4) s += p[(long)j * H];
-    }
-  red[rg][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (rg == 0 && n < H && e1 > e0)
-    atomicAdd(dbeta + (long)c * H + n, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
