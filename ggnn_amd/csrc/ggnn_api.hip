@@ -1226,7 +1226,7 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
   for (int i = 0; i < nheads; ++i) {
     const ggnn_output_head& hd = heads[i];
     const int o = hd.o, op = (o + 3) & ~3;
-    const dim3 g((unsigned)std::min<long>(512, (rows + 7) / 8));
+    const dim3 g((unsigned)std::min<long>(256, (rows + 15) / 16));  // (bias atomics: one per column per block)
 #define HDZ(NI_)                                                                                                  \
   hipLaunchKernelGGL(k_head_dz<NI_>, g, dim3(256), 0, s, hd.probs, hd.labels, rows, o, op, 1.0f / target_num, d_loss, \
                      dZ + L.off[i], Ot, hd.d_bias)

@@ -242,10 +242,11 @@ __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, co
 #pragma unroll
   for (int i = 0; i < NI; ++i) part[i] = 0.f;
   const long stride = (long)gridDim.x * 4;
-  for (long r0 = (long)blockIdx.x * 4 + w; r0 < rows; r0 += 2 * stride) {
-    float pv[2][NI], yv[2][NI];
+  constexpr int RP = 4;  // rows per wave and iteration, loads in flight together
+  for (long r0 = (long)blockIdx.x * 4 + w; r0 < rows; r0 += RP * stride) {
+    float pv[RP][NI], yv[RP][NI];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < RP; ++u) {
       const long r = r0 + u * stride;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -256,7 +257,7 @@ __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, co
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < RP; ++u) {
       const long r = r0 + u * stride;
       if (r >= rows) break;
       float sy = 0.f;
