@@ -633,11 +633,17 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
   a.H = (int)H;
+  // K chunks are sized by the tiles of T-summed problems: under edge dropout
+  // the dW problem runs per timestep (nt * C tiles of one timestep each), and
+  // counting those tiles halved the chunk count, doubling the slices of the
+  // GRU-gradient workgroups (all nt timesteps each), which then set the launch
+  // time (measured +0.27 ms per step at config 3 with keep 0.9)
+  const long tiles_eq = c.ed ? tiles - (long)(nt - 1) * c.C * a.p[np - 1].tiles_b : tiles;
   if (big) {
     // one workgroup per CU (128 KiB LDS ring): the largest K chunk that still
     // gives >= 7/8 of the CUs a tile-chunk
     int KC = 8192;
-    while (KC > 128 && ((N % KC) != 0 || (long)tiles * (N / KC) < 224)) KC /= 2;
+    while (KC > 128 && ((N % KC) != 0 || tiles_eq * (N / KC) < 224)) KC /= 2;
     if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
     a.KC = KC;
     a.nchunks = (int)(N / KC);
@@ -647,7 +653,7 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   }
   int KC = 4096;
   while (KC > 32 && (N % KC) != 0) KC /= 2;
-  while (KC > 256 && (long)tiles * (N / KC) < 256) KC /= 2;
+  while (KC > 256 && tiles_eq * (N / KC) < 256) KC /= 2;
   if (N % KC) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
   a.KC = KC;
   a.nchunks = (int)(N / KC);
@@ -781,6 +787,7 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
     if (a.count == PACK_MAXJ) flush();
     PackJob& J = a.j[a.count];
+    if (mode == 2 && drop) n /= 4;  // (one thread per 4-row quad, k_pack_multi)
     J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop;
     a.blk_begin[a.count++] = nb;
     nb += (int)((n + 255) / 256);

@@ -354,12 +354,20 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     return;
   }
   if (J.copy == 2) {  // fp32 copy of W [C][H][H] (H = J.K), edge-dropout mask of timestep J.t when J.drop
-    float x = J.S[q];
-    if (J.drop) {
-      const int H = J.K, wi = (int)((q / H) % H), wj = (int)(q % H), c = (int)(q / ((long)H * H));
-      x = drop_apply(a.dr, u4_get(edge_words(a.dr, c, wi, wj, J.t), wi & 3), x);
+    if (!J.drop) {
+      ((float*)J.out)[q] = J.S[q];
+      return;
     }
-    ((float*)J.out)[q] = x;
+    // masked: one thread per 4-row quad of one column (J.total = C*H*H / 4),
+    // whose 4 masks are the 4 words of one Philox block
+    const int H = J.K, hq = H >> 2;
+    const int wj = (int)(q % H), iq = (int)((q / H) % hq), c = (int)(q / ((long)H * hq));
+    const uint4 w = edge_words(a.dr, c, 4 * iq, wj, J.t);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long e = ((long)c * H + 4 * iq + u) * H + wj;
+      ((float*)J.out)[e] = drop_apply(a.dr, u4_get(w, u), J.S[e]);
+    }
     return;
   }
   const int per = (J.N / 32) * (J.K / 16) * 64;  // fragment-lanes per matrix
@@ -374,10 +382,14 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) x[e] = J.trans ? Sb[(long)n * J.ldS + k0 + e] : Sb[(long)(k0 + e) * J.ldS + n];
   if (J.drop) {
+    if (!J.trans) {  // rows k0 .. k0 + 7 of column n: two quads, two Philox blocks
+      const uint4 w0 = edge_words(a.dr, mat, k0, n, J.t), w1 = edge_words(a.dr, mat, k0 + 4, n, J.t);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int wi = J.trans ? n : k0 + e, wj = J.trans ? k0 + e : n;
-      x[e] = drop_apply(a.dr, u4_get(edge_words(a.dr, mat, wi, wj, J.t), wi & 3), x[e]);
+      for (int e = 0; e < 8; ++e) x[e] = drop_apply(a.dr, u4_get(e < 4 ? w0 : w1, e & 3), x[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        x[e] = drop_apply(a.dr, u4_get(edge_words(a.dr, mat, n, k0 + e, J.t), n & 3), x[e]);
     }
   }
   *(uint4*)(ob + (size_t)r * 8) = pk8<F16>(x);
