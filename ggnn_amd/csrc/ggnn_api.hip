@@ -398,7 +398,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
                        hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), P<u16>(ws, L.hT), N, c.H);
   } else if (!dense || (!SPLIT && !fused)) {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H,
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N / 4 * H)), dim3(256), 0, s, h0, c.vin, c.V, c.H,
                        dense ? (float*)nullptr : hf0, SPLIT ? (u16*)nullptr : P<u16>(ws, L.hb[0]), N,
                        (int)Prec<PREC>::f16, kNoDrop, 0, (const uint32_t*)nullptr);
   }
@@ -535,7 +535,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const bool in_place = dense && !c.sd;
   if (!in_place) {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
+    hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N / 4 * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
                        c.sdrop, c.T - 1, gmax);
   }
   for (int t = c.T - 1; t >= 0; --t) {

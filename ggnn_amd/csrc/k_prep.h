@@ -99,17 +99,26 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
 // dropout mask of timestep t is applied (backward: dL/dh_T -> dL/dh'_{T-1}).
 __global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H, float* __restrict__ hf,
                             u16* __restrict__ hb, long N, int f16, Drop dr, int t, const uint32_t* gmax) {
-  const long total = N * H;
+  // one thread per (4-row quad, column): V is a multiple of 4, so a quad lies
+  // inside one graph and its 4 state-dropout masks are one Philox block
+  const long total = N / 4 * H;
   const float sc = gscale(gmax);  // backward staging of dL/dh_T: the gradient scale (ggnn_common.h)
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const long row = q / H;
-    const int col = q % H;
-    const long g = row / V;
-    const int i = row % V;
-    float x = (i < vin) ? h0[(g * vin + i) * H + col] * sc : 0.0f;
-    if (dr.thr) x = drop_apply(dr, u4_get(state_words(dr, (int)g, i, col, t), i & 3), x);
-    if (hf) hf[q] = x;
-    if (hb) hb[q] = f16 ? to_limb<true>(x) : to_limb<false>(x);
+    const long rq = q / H;
+    const int col = (int)(q - rq * H);
+    const long row0 = rq * 4, g = row0 / V;
+    const int i0 = (int)(row0 - g * V);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (dr.thr) w = state_words(dr, (int)g, i0, col, t);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      const long e = (row0 + u) * H + col;
+      float x = (i < vin) ? h0[(g * vin + i) * H + col] * sc : 0.0f;
+      if (dr.thr) x = drop_apply(dr, u4_get(w, u), x);
+      if (hf) hf[e] = x;
+      if (hb) hb[e] = f16 ? to_limb<true>(x) : to_limb<false>(x);
+    }
   }
 }
 
