@@ -287,7 +287,7 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     if (int e = gg_launch<PREC>(cd, false, true, false, K_GRU_FWD, s)) return e;
     {
       Prof p(K_GRU_FWD, s);
-      hipLaunchKernelGGL(k_gen_blend, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
+      hipLaunchKernelGGL(k_gen_blend, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
                          P<const float>(ws, hin), P<const float>(ws, L.cc(t)), hout, N, c.H, c.vin, c.sdrop, t);
     }
   }
@@ -327,7 +327,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(N * H / 4 + 1), 1024)), dim3(256), 0, s, dhT, N * H,
                        P<uint32_t>(ws, L.gmax));
-    hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d(N * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
+    hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
                        gmax);
   }
   // split-K chunk of the weight-gradient products over the N rows
@@ -421,7 +421,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
     {
       Prof p(K_PROP_BWD, s);
-      hipLaunchKernelGGL(k_gen_delta, dim3(grid1d(N * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
+      hipLaunchKernelGGL(k_gen_delta, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
                          c.sdrop, t - 1, gmax, t == 0 ? 1 : 0);
     }
   }

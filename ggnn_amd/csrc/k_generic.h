@@ -119,20 +119,43 @@ __global__ void k_gen_rh(const float* __restrict__ G, const float* __restrict__ 
     rh[e] = G[row * 2 * H + k] * h[e];
   }
 }
+// State-dropout element-wise kernels: one thread per (graph, row quad,
+// column) -- rows unpadded (v = vin), so a graph's last quad may be partial --
+// drawing the quad's 4 masks as one Philox block (counter (i >> 2, k, g, t),
+// word i & 3), with one division pair per 4 elements.
+struct QuadIdx {
+  long row0;  // first row of the quad
+  int g, i0, k, nr;  // graph, first node, column, rows in the quad
+};
+DEV bool quad_idx(long q, int H, int v, long b, QuadIdx& x) {
+  const int vq = (v + 3) >> 2;
+  if (q >= b * vq * H) return false;
+  const long r = q / H;
+  x.k = (int)(q - r * H);
+  x.g = (int)(r / vq);
+  x.i0 = (int)(r - (long)x.g * vq) * 4;
+  x.nr = min(4, v - x.i0);
+  x.row0 = (long)x.g * v + x.i0;
+  return true;
+}
 // h' = u h + (1 - u) c, then the DropoutWrapper state dropout of timestep t
 __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict__ h, const float* __restrict__ cc,
                             float* __restrict__ hout, long N, int H, int v, Drop sd, int t) {
-  const long total = N * H;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long row = e / H;
-    const int k = (int)(e % H);
-    const float u = G[row * 2 * H + H + k];
-    float x = u * h[e] + (1.0f - u) * cc[e];
-    if (sd.thr) {
-      const int g = (int)(row / v), i = (int)(row % v);
-      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, t), i & 3), x);
+  const long b = N / v, total = b * ((v + 3) >> 2) * H;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    QuadIdx x;
+    quad_idx(q, H, v, b, x);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (sd.thr) w = state_words(sd, x.g, x.i0, x.k, t);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u >= x.nr) break;
+      const long row = x.row0 + u, e = row * H + x.k;
+      const float ug = G[row * 2 * H + H + x.k];
+      float y = ug * h[e] + (1.0f - ug) * cc[e];
+      if (sd.thr) y = drop_apply(sd, u4_get(w, u), y);
+      hout[e] = y;
     }
-    hout[e] = x;
   }
 }
 
@@ -189,32 +212,41 @@ __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh,
 // gradient unscale on the last step, else 1)
 __global__ void k_gen_delta(const float* __restrict__ DXH, float* __restrict__ out, long N, int H, int v, Drop sd,
                             int tm, const uint32_t* __restrict__ gmax, int unscale) {
-  const long total = N * H;
+  const long b = N / v, total = b * ((v + 3) >> 2) * H;
   const float osc = unscale ? gunscale(gmax) : 1.0f;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long row = e / H;
-    const int k = (int)(e % H);
-    float x = DXH[row * 2 * H + H + k] * osc;
-    if (sd.thr && tm >= 0) {
-      const int g = (int)(row / v), i = (int)(row % v);
-      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, tm), i & 3), x);
+  const bool drop = sd.thr && tm >= 0;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    QuadIdx x;
+    quad_idx(q, H, v, b, x);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (drop) w = state_words(sd, x.g, x.i0, x.k, tm);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u >= x.nr) break;
+      const long row = x.row0 + u;
+      float y = DXH[row * 2 * H + H + x.k] * osc;
+      if (drop) y = drop_apply(sd, u4_get(w, u), y);
+      out[row * H + x.k] = y;
     }
-    out[e] = x;
   }
 }
 // dL/dh_T staging: delta = S * dL/dh_T (gradient scale), state dropout of T-1
 __global__ void k_gen_delta0(const float* __restrict__ dhT, float* __restrict__ out, long N, int H, int v, Drop sd,
                              int tm, const uint32_t* __restrict__ gmax) {
-  const long total = N * H;
+  const long b = N / v, total = b * ((v + 3) >> 2) * H;
   const float sc = gscale(gmax);
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    float x = dhT[e] * sc;
-    if (sd.thr) {
-      const long row = e / H;
-      const int k = (int)(e % H);
-      const int g = (int)(row / v), i = (int)(row % v);
-      x = drop_apply(sd, u4_get(state_words(sd, g, i, k, tm), i & 3), x);
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    QuadIdx x;
+    quad_idx(q, H, v, b, x);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (sd.thr) w = state_words(sd, x.g, x.i0, x.k, tm);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u >= x.nr) break;
+      const long e = (x.row0 + u) * H + x.k;
+      float y = dhT[e] * sc;
+      if (sd.thr) y = drop_apply(sd, u4_get(w, u), y);
+      out[e] = y;
     }
-    out[e] = x;
   }
 }
