@@ -309,15 +309,17 @@ def test_errors_are_raised_not_ignored():
     eng.dims(1, 200, 1)
 
 
-def test_drop_in_model_on_reference_dev_batches():
+@pytest.mark.parametrize("hidden", [128, 400])
+def test_drop_in_model_on_reference_dev_batches(hidden):
     """DenseGGNNChemModel fed with real WSJ dev minibatches (golden fixture of
     the reference's own data, C = 2*46 = 92 channels): forward and autograd
-    backward against the oracle, fp32 mode."""
+    backward against the oracle, fp32 mode; hidden 128 on the specialised
+    kernels, the reference's default 400 on the general path."""
     torch = _torch()
     from ggnn_amd.model import DenseGGNNChemModel
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
     data = json.loads(str(g["raw_json"]))
-    m = DenseGGNNChemModel(params={"hidden_size": 128, "num_timesteps": 3, "batch_size": 8},
+    m = DenseGGNNChemModel(params={"hidden_size": hidden, "num_timesteps": 3, "batch_size": 8},
                            num_edge_types=int(g["num_edge_types"]), output_size_edges=int(g["output_size_edges"]),
                            pos_size=int(g["pos_size"]), bucket_max_nodes=int(g["bucket_max_nodes"]),
                            precision="fp32")
@@ -329,7 +331,7 @@ def test_drop_in_model_on_reference_dev_batches():
     for fd in feeds[:3]:
         m.feed(fd)
         b, v = fd["num_graphs"], fd["num_vertices"]
-        h0 = rng.uniform(-0.5, 0.5, (b, v, 128)).astype(np.float32)
+        h0 = rng.uniform(-0.5, 0.5, (b, v, hidden)).astype(np.float32)
         h0_t = torch.from_numpy(h0).to(m.device).requires_grad_(True)
         out = m.compute_final_node_representations(h0_t)
         A64 = np.asarray(fd["adjacency_matrix"], np.float64)
