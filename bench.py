@@ -291,7 +291,7 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10,
     return out
 
 
-def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
+def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
     """Side measurement (SURVEY §8f rank 3 / configs[4] shapes): the fwd+bwd
     step on dependency-tree graphs with the real btb label set (std->nivre,
     E = 46 -> C = 92 channels, most of them empty per graph), with empty-channel
@@ -318,7 +318,7 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
     dhT = torch.from_numpy(rng.standard_normal((b, v, h)).astype(np.float32)).to(dev)
     res = {"workload": "b=%d dependency trees, v=%d, hidden=%d, E=%d (C=%d), T=%d, fwd+bwd" % (
         b, v, h, E, C, T), "nonempty_channels_per_graph_mean": float(np.mean(occ))}
-    for skip in (True, False):
+    for skip in ((True, False) if both else (True,)):
         eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision="fp32", skip_empty_channels=skip)
         eng.set_adjacency_edges(graphs, v, E)
         grads = FlatGradients(h, C, True, device=dev)
@@ -335,7 +335,12 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5):
         res["skip" if skip else "dense"] = {"ms_per_step": ms, "graphs_per_s": b / (ms * 1e-3)}
         del eng, grads, gv, out
         torch.cuda.empty_cache()
-    res["speedup"] = res["dense"]["ms_per_step"] / res["skip"]["ms_per_step"]
+    if both:
+        res["speedup"] = res["dense"]["ms_per_step"] / res["skip"]["ms_per_step"]
+        # the reference's own model on these graphs: hidden_size 400, num_timesteps 4
+        # (chem_tensorflow.py:95-96, configs[0] / configs[4]), general path
+        r4 = real_density_side(dev, b, v, 400, E, 4, steps, both=False)
+        res["reference_defaults_h400_T4"] = {"workload": r4["workload"], **r4["skip"]}
     return res
 
 
