@@ -131,15 +131,15 @@ static int gemm_kernel_env() {
   return v;
 }
 
-// ring depth: 2 slots (64 KiB: two workgroups per CU) by default -- measured
-// 1.4-2x faster than the 4-slot ring (one workgroup per CU) on every probe
-// shape (tools/gemm_ring_probe.py): a second workgroup's MFMAs cover one's
-// prologue, barriers and epilogue better than deeper prefetch does;
-// GGNN_RING_NBUF=4 selects the 4-slot ring
-static int ring_nbuf_env() {
+// ring depth: 2 slots (64 KiB: two workgroups per CU) -- measured 1.4-2x
+// faster than a 4-slot ring (one workgroup per CU) on every probe shape
+// (tools/gemm_ring_probe.py): a second workgroup's MFMAs cover one's prologue,
+// barriers and epilogue better than deeper prefetch does.
+// GGNN_RING_SMALL=0 keeps 128-row tiles for small-M products (A/B)
+static int ring_small_env() {
   static const int v = [] {
-    const char* e = getenv("GGNN_RING_NBUF");
-    return e ? atoi(e) : 2;
+    const char* e = getenv("GGNN_RING_SMALL");
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -151,27 +151,34 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
   if ((g_gemm_force == 2 || (g_gemm_force == 0 && gemm_kernel_env() == 0)) && ring_ok(a, A16, AKC, BKC)) {
-    const int tn = (a.N + 127) / 128, tm = (a.M + 127) / 128;
+    // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
+    // per-(graph, channel) products of v = 30 sentence graphs), 128 otherwise
+    const bool small = AKC && a.M <= 64 && ring_small_env();
+    const int bm = small ? 32 : 128;
+    const int tn = (a.N + 127) / 128, tm = (a.M + bm - 1) / bm;
     const long nwg = (long)tn * tm * a.Z;
     if (nwg > 0x7fffffffL) return fail(GGNN_EINVAL, "k_gemm_ring: grid too large");
     const dim3 grid((unsigned)nwg);
     Prof p(kind, s);
     const bool sc = a.scA != 1.0f || a.scB != 1.0f;
-    const bool nb2 = ring_nbuf_env() == 2;
-#define GGR(A16_, AKC_, BKC_)                                                                              \
+#define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
-    if (sc && nb2) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2>), grid, dim3(256), 0, s, a, tm, tn); \
-    else if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 4>), grid, dim3(256), 0, s, a, tm, tn); \
-    else if (nb2) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2>), grid, dim3(256), 0, s, a, tm, tn); \
-    else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 4>), grid, dim3(256), 0, s, a, tm, tn);    \
+    if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
+    else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);    \
+  } while (0)
+#define GGR(A16_, AKC_, BKC_)              \
+  do {                                     \
+    if (small) GGR1(A16_, AKC_, BKC_, 32);  \
+    else GGR1(A16_, AKC_, BKC_, 128);       \
   } while (0)
     if (A16 && !BKC) GGR(true, true, false);
     else if (A16) return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
     else if (AKC && !BKC) GGR(false, true, false);
     else if (AKC && BKC) GGR(false, true, true);
-    else if (!AKC && !BKC) GGR(false, false, false);
+    else if (!AKC && !BKC) GGR1(false, false, false, 128);
     else return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
 #undef GGR
+#undef GGR1
     return GGNN_OK;
   }
   // 64 x 64 block tiles: measured faster than the 128 x 64 / 128 x 128

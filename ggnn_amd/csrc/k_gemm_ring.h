@@ -78,16 +78,26 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
   nt = u / gs;
 }
 
-template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF>
+// BMT: block rows, 128 (4 waves in 2 x 2, 64 x 64 each) or 32 (4 waves in
+// 1 x 4, 32 x 32 each: products whose M is one small graph's node count, e.g.
+// v = 30 sentence graphs, where a 128-row tile would spend 3/4 of its MFMAs and
+// A bytes on padding rows; k-contiguous A only)
+template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT>
 __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   static_assert(!A16 || AKC, "16-bit A operands are k-contiguous");
+  static_assert(BMT == 128 || (BMT == 32 && AKC), "32-row tiles: k-contiguous A only");
+  constexpr int BM = BMT;
+  constexpr int WMW = BMT == 128 ? 2 : 1, WNW = 4 / WMW;  // wave grid
+  constexpr int AM = BMT / (32 * WMW), AN = BN / (32 * WNW);  // accumulators per wave
   constexpr int ES = A16 ? 2 : 4;                       // A element bytes
-  constexpr int AB = A16 ? BM * BK * 2 : BM * BK * 4;  // A slice image bytes
+  constexpr int AB = BM * BK * ES;                      // A slice image bytes
   constexpr int BB = BN * BK * 4;
-  constexpr int SB = AB + BB;
-  constexpr int GA = AB / 1024 / 4, GB = BB / 1024 / 4;  // DMA instructions per wave per slice
+  constexpr int NA = AB / 1024;                         // A wave-instructions per slice
+  constexpr int GA = (NA + 3) / 4, GB = BB / 1024 / 4;  // DMA instructions per wave per slice
+  constexpr bool AJUNK = GA * 4 > NA;                   // waves past the A image DMA a dummy chunk
+  constexpr int SB = AB + BB + (AJUNK ? 1024 : 0);
   constexpr int GPW = GA + GB;
   // one __shared__ object per ring slot, addressed with compile-time indices
   // (NBUF = 4: three slices in flight, one workgroup per CU; NBUF = 2: one
@@ -96,7 +106,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   __shared__ __attribute__((aligned(16))) char s0[SB], s1[SB], s2[NBUF > 2 ? SB : 16], s3[NBUF > 2 ? SB : 16];
   auto slot = [&](int u) -> char* { return u == 0 ? s0 : u == 1 ? s1 : u == 2 ? s2 : s3; };
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
-  const int wm = w & 1, wn = w >> 1;
+  const int wm = w % WMW, wn = w / WMW;
   int z, mt, ntile;
   ring_tile(gridDim.x, tm, tn, z, mt, ntile);
   if (z >= a.Z) return;
@@ -182,7 +192,8 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
     for (int g = 0; g < GA; ++g) {
       const int k = kk0 + ka[g];
       const char* src = AKC ? pa[g] + (long)k * ES : pa[g] + (long)k * a.sAk * 4;
-      glds16_asm(k < keff ? src : zero, buf + (g * 4 + w) * 1024);
+      const int qi = g * 4 + w;  // A wave-instruction index (>= NA: dummy into the junk chunk)
+      glds16_asm(k < keff ? src : zero, buf + (AJUNK && qi >= NA ? AB + BB : qi * 1024));
     }
 #pragma unroll
     for (int g = 0; g < GB; ++g) {
@@ -192,11 +203,11 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[AM][AN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < AM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = splat(0.f);
+    for (int j = 0; j < AN; ++j) acc[i][j] = splat(0.f);
 
   // ---- MFMAs of the slice in ring slot `buf` (straight-line: the LDS reads
   // of both k-steps issue together)
@@ -207,10 +218,10 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int k0 = 16 * s + 8 * hh;
-      frag ah[2], al[2], bh[2], bl[2];
+      frag ah[AM], al[AM], bh[AN], bl[AN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wm * 64 + i * 32 + l32;
+      for (int i = 0; i < AM; ++i) {
+        const int r = wm * AM * 32 + i * 32 + l32;
         if constexpr (A16) {
           ah[i] = *(const frag*)(ia + kc16_off(r, k0 >> 3));
           al[i] = ah[i];
@@ -225,8 +236,8 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn * 64 + j * 32 + l32;
+      for (int j = 0; j < AN; ++j) {
+        const int r = wn * AN * 32 + j * 32 + l32;
         float x[8];
         rd8<BKC>(ib, r, k0, x);
         if constexpr (SCALE)
@@ -236,9 +247,9 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
         bl[j] = SPLIT ? pk8_lo<true>(x) : bh[j];
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < AM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < AN; ++j) {
           if constexpr (A16) mma_xa<PREC>(acc[i][j], ah[i], bh[j], bl[j]);
           else mma<PREC>(acc[i][j], ah[i], al[i], bh[j], bl[j]);
         }
@@ -268,17 +279,17 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
   const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + 32 * j + l32;
+  for (int j = 0; j < AN; ++j) {
+    const int n = n0 + wn * AN * 32 + 32 * j + l32;
     float cs = 0.f;
     if (n < a.N) {
       const float bn = bias ? bias[n] : 0.f;
       const bool hi_n = a.Nsplit && n >= a.Nsplit;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < AM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + 32 * i + acc_row(r, hh);
+          const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
           if (m >= a.M) continue;
           float x = a.alpha * acc[i][j][r] + bn;
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
