@@ -372,14 +372,18 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.M = (int)N; a.N = (int)(2 * H); a.K = (int)(2 * H);
       if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
     }
-    // GRU weight gradients: split-K over row chunks, atomics
+    // GRU weight gradients: split-K over row chunks, atomics.  The weight
+    // gradients take single f16 operands in the fp32-parity mode, as the fast
+    // path's k_wgrad256 does (measured <= 3.7e-4 normalised against float64;
+    // the dh / dX chain keeps the split limbs): a third of the MFMAs
+    constexpr int WPREC = Prec<PREC>::split ? PREC_F16 : PREC;
     auto wg = [&](const float* Aop, const float* Bop, long ldB, int Nn, float* out, long ldO) {
       GemmArgs a = gg_args();
       a.A = Aop; a.sAp = KC * H; a.sAm = 1; a.sAk = H;
       a.B = Bop; a.sBp = KC * ldB; a.sBk = ldB; a.sBn = 1;
       a.D = out; a.sDm = ldO; a.sDn = 1; a.mode = GG_ATOMIC;
       a.Z = nkc; a.M = (int)H; a.N = Nn; a.K = (int)KC; a.Ktot = N; a.sKp = KC;
-      return gg_launch<PREC>(a, false, false, false, K_WGRAD, s);
+      return gg_launch<WPREC>(a, false, false, false, K_WGRAD, s);
     };
     if (int e = wg(P<float>(ws, L.x(t)), DZC, H, (int)H, dWc, H)) return e;
     if (int e = wg(P<float>(ws, L.rh(t)), DZC, H, (int)H, dWc + H * H, H)) return e;
@@ -419,7 +423,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.mode = chunked ? GG_ATOMIC : c.ed ? GG_STORE : GG_ADD;
       a.tl = P<int>(adj, AL.cgc); a.ts = AL.gch + 1; a.zdiv = AL.nch;  // z = (channel, chunk of its graphs)
       a.Z = (int)C * AL.nch; a.M = (int)H; a.N = (int)H; a.K = (int)v;
-      if (int e = gg_launch<PREC>(a, false, false, false, K_WGRAD, s)) return e;
+      if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       if (c.ed)
         hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * H * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,

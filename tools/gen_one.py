@@ -1,4 +1,4 @@
-"""One general-path shape under the profiler: b v h C T [trees]."""
+"""One general-path shape under the profiler: b v h C T [trees] [generic]."""
 import json
 import os
 import sys
@@ -8,4 +8,5 @@ from generic_probe import run  # noqa: E402
 
 if __name__ == "__main__":
     b, v, h, C, T = (int(x) for x in sys.argv[1:6])
-    print(json.dumps(run(b, v, h, C, T, False, trees=len(sys.argv) > 6 and sys.argv[6] == "trees")))
+    flags = sys.argv[6:]
+    print(json.dumps(run(b, v, h, C, T, "generic" in flags, trees="trees" in flags, steps=10)))
