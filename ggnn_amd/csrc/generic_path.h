@@ -448,7 +448,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     add(dWc, 2 * H * H);
     add(dbc, H);
     if (use_bias) add(dbeta, C * H);
-    hipLaunchKernelGGL(k_unscale_multi, dim3(128, nj), dim3(256), 0, s, j, gmax);
+    hipLaunchKernelGGL(k_unscale_multi, dim3(512, nj), dim3(256), 0, s, j, gmax);
   }
   LAUNCHCHK();
   return GGNN_OK;

@@ -580,7 +580,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     add(dWc, 2 * H * H);
     add(dbc, H);
     if (use_bias) add(dbeta, (long)c.C * H);
-    hipLaunchKernelGGL(k_unscale_multi, dim3(128, nj), dim3(256), 0, s, j, gmax);
+    hipLaunchKernelGGL(k_unscale_multi, dim3(512, nj), dim3(256), 0, s, j, gmax);
   }
 
   LAUNCHCHK();

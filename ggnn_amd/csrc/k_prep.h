@@ -460,5 +460,15 @@ __global__ void __launch_bounds__(256) k_unscale_multi(ZeroJobs a, const uint32_
   const long n = a.n[blockIdx.y];
   const float sc = gunscale(gmax);
   const long stride = (long)gridDim.x * 256;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] *= sc;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if ((((unsigned long)p) & 15) == 0) {  // 16-byte pieces, then the tail
+    for (; 4 * i + 3 < n; i += stride) {
+      float4 v = *(float4*)(p + 4 * i);
+      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+      *(float4*)(p + 4 * i) = v;
+    }
+    for (long k = (n & ~3L) + (long)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) p[k] *= sc;
+  } else {
+    for (; i < n; i += stride) p[i] *= sc;
+  }
 }
