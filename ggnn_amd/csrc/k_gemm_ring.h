@@ -112,6 +112,10 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   if (z >= a.Z) return;
   if (a.zmask && !a.zmask[z]) return;
   const int n0 = ntile * BN, m0 = mt * BM;
+  // a wave whose whole row or column slice lies past M / N (the last tile of
+  // N = 400: 16 of its 128 columns valid) still moves its share of every slice
+  // and meets every barrier, but reads no fragments and issues no MFMAs
+  const bool live = __builtin_amdgcn_readfirstlane((int)(n0 + wn * AN * 32 < a.N && m0 + wm * AM * 32 < a.M));
   const int kc = (a.K + BK - 1) / BK;
   const int zp = z / a.zdiv, zq = z % a.zdiv;
   const int nterms = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
@@ -270,10 +274,11 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
         if (it + NBUF - 1 < nit) stage(it + NBUF - 1, slot((u + NBUF - 1) % NBUF));
-        compute(slot(u));
+        if (live) compute(slot(u));
       }
     }
   }
+  if (!live) return;  // nothing of this wave's to store (no barrier follows)
 
   // ---- epilogue (as k_gemm)
   const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
