@@ -55,41 +55,100 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
                                                   u16* __restrict__ Ab, u16* __restrict__ AbT,
                                                   u16* __restrict__ deg) {
   constexpr int P = V + 8;           // row pitch (u16): 16-B aligned rows, odd dword pitch / 4
-  __shared__ __attribute__((aligned(16))) u16 t[V][P];   // A[i][j]
   __shared__ __attribute__((aligned(16))) u16 tt[V][P];  // A[j][i] (transposed)
   const long tile = blockIdx.x;  // g*C + c
   const float* src = A + tile * (long)vin * vin;
-  if (vin == V) {  // unpadded: 16-byte loads
-    for (int q = threadIdx.x; q < V * V / 4; q += 256) {
-      const int i = q / (V / 4), j = (q % (V / 4)) * 4;
-      const float4 x = *(const float4*)(src + i * V + j);
-      const u16 a0 = to_limb<F16>(x.x), a1 = to_limb<F16>(x.y), a2 = to_limb<F16>(x.z), a3 = to_limb<F16>(x.w);
-      *(uint2*)&t[i][j] = make_uint2(a0 | ((uint32_t)a1 << 16), a2 | ((uint32_t)a3 << 16));
-      tt[j][i] = a0; tt[j + 1][i] = a1; tt[j + 2][i] = a2; tt[j + 3][i] = a3;
-    }
-  } else {
-    for (int q = threadIdx.x; q < V * V; q += 256) {
-      const int i = q / V, j = q % V;
-      const u16 a = to_limb<F16>((i < vin && j < vin) ? src[i * vin + j] : 0.0f);
-      t[i][j] = a;
-      tt[j][i] = a;
-    }
-  }
-  __syncthreads();
   u16* ab = Ab + tile * V * V;
   u16* at = AbT + tile * V * V;
+  if (vin == V) {
+    // unpadded: one unit = 4 rows x the 8 columns of one Ab output chunk
+    // (columns c0..c0+3 and c0+8..c0+11, c0 = g16 + 4 h), all loads of a
+    // thread issued before any use; Ab straight from registers, A^T through
+    // LDS as 4-row uint2 pieces, deg as a row sum over the V/8 lanes of a row
+    // group (exact for the reference's 0/1 adjacency)
+    constexpr int SL = V / 8;                  // units (lanes) per 4-row group
+    constexpr int U = V * V / 32;              // units per tile
+    constexpr int UPT = (U + 255) / 256;       // units per thread
+    float4 x[UPT][4][2];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int u = threadIdx.x + k * 256;
+      if (U % 256 == 0 || u < U) {
+        const int i = (u / SL) * 4, sl = u % SL, c0 = (sl >> 1) * 16 + (sl & 1) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[k][r][0] = *(const float4*)(src + (i + r) * V + c0);
+          x[k][r][1] = *(const float4*)(src + (i + r) * V + c0 + 8);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[k][r][0] = x[k][r][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int u = threadIdx.x + k * 256;
+      const bool act = U % 256 == 0 || u < U;
+      const int i = (u / SL) * 4, sl = u % SL, c0 = (sl >> 1) * 16 + (sl & 1) * 4;
+      u16 a[4][8];
+      float rs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v8[8] = {x[k][r][0].x, x[k][r][0].y, x[k][r][0].z, x[k][r][0].w,
+                             x[k][r][1].x, x[k][r][1].y, x[k][r][1].z, x[k][r][1].w};
+        rs[r] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[r][e] = to_limb<F16>(v8[e]);
+          rs[r] += from_limb<F16>(a[r][e]);
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *(uint4*)(ab + (i + r) * V + (sl >> 1) * 16 + (sl & 1) * 8) =
+              make_uint4(a[r][0] | ((uint32_t)a[r][1] << 16), a[r][2] | ((uint32_t)a[r][3] << 16),
+                         a[r][4] | ((uint32_t)a[r][5] << 16), a[r][6] | ((uint32_t)a[r][7] << 16));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int j = c0 + (e & 3) + (e >> 2) * 8;
+          *(uint2*)&tt[j][i] = make_uint2(a[0][e] | ((uint32_t)a[1][e] << 16), a[2][e] | ((uint32_t)a[3][e] << 16));
+        }
+      }
+      // row sums over the SL lanes of this row group (contiguous, SL | 64)
+#pragma unroll
+      for (int o = 1; o < SL; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rs[r] += __shfl_xor(rs[r], o);
+      if (act && sl == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) deg[tile * V + i + r] = to_limb<F16>(rs[r]);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < V * V / 8; q += 256) {
+      const int i = q / (V / 8), p = (q % (V / 8)) * 8;
+      *(uint4*)(at + i * V + p) = *(const uint4*)&tt[i][p];
+    }
+    return;
+  }
+  // padded graphs (vin < V): element-wise, Ab's permuted column order
+  // (inside every 16-column group the 8-byte chunks 1 and 2 swapped) applied
+  // on the store
+  for (int q = threadIdx.x; q < V * V; q += 256) {
+    const int i = q / V, j = q % V;
+    const u16 a = to_limb<F16>((i < vin && j < vin) ? src[i * vin + j] : 0.0f);
+    const int jj = (j & ~15) | (((j >> 2) & 3) == 1 ? (j & 3) + 8 : ((j >> 2) & 3) == 2 ? (j & 3) + 4 : (j & 15));
+    ab[i * V + jj] = a;
+    tt[j][i] = a;
+  }
+  __syncthreads();
   for (int q = threadIdx.x; q < V * V / 8; q += 256) {
-    const int i = q / (V / 8), p = (q % (V / 8)) * 8;  // 8 outputs [p, p+8) of row i
-    // Ab column order: inside every 16-column group the 8-byte chunks 1 and 2
-    // are swapped (p..p+7 = columns g+0..3, g+8..11 or g+4..7, g+12..15)
-    const int g16 = p & ~15, c0 = g16 + ((p & 8) ? 4 : 0);
-    const uint2 lo = *(const uint2*)&t[i][c0], hi = *(const uint2*)&t[i][c0 + 8];
-    *(uint4*)(ab + i * V + p) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    const int i = q / (V / 8), p = (q % (V / 8)) * 8;
     *(uint4*)(at + i * V + p) = *(const uint4*)&tt[i][p];
   }
   if (threadIdx.x < V) {
     float s = 0.f;
-    for (int j = 0; j < V; ++j) s += from_limb<F16>(t[threadIdx.x][j]);
+    for (int j = 0; j < V; ++j) s += from_limb<F16>(tt[j][threadIdx.x]);
     deg[tile * V + threadIdx.x] = to_limb<F16>(s);
   }
 }

@@ -490,7 +490,7 @@ def _random_graphs(rng, b, v, E, n_edges):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-@pytest.mark.parametrize("b,v,E", [(3, 20, 2), (4, 64, 4), (2, 128, 4), (5, 50, 46)])
+@pytest.mark.parametrize("b,v,E", [(3, 20, 2), (3, 32, 2), (4, 64, 4), (2, 128, 4), (5, 50, 46)])
 def test_adjacency_from_edges_is_byte_identical(b, v, E, precision):
     """ggnn_set_adjacency_edges stages exactly the bytes that ggnn_set_adjacency
     stages from the reference's dense graph_to_adj_mat_bd feed."""
