@@ -438,6 +438,11 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     fa.T = c.T;
     fa.vsh = c.vsh;
     fa.sd = c.sdrop;
+    static const int skew = [] {
+      const char* e = getenv("GGNN_FWD_SKEW");
+      return e ? std::max(0, atoi(e)) : 0;
+    }();
+    fa.skew = skew;
     {
       Prof p(K_FWD_FUSED, s);
       hipLaunchKernelGGL(k_fwd_fused<PREC>, dim3(c.b), dim3(512), 0, s, fa);

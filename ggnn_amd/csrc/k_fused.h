@@ -54,6 +54,7 @@ struct FusedFwdArgs {
   long sw, s4;
   int C, T, vsh;
   Drop sd;
+  int skew;                     // experiment knob (GGNN_FWD_SKEW): odd graphs start skew x s_sleep(127) late
 };
 
 // PREC: PREC_SPLIT (fp32-parity: f16 hi/lo limb images, 3 products) or a
@@ -80,6 +81,8 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
   auto slot_lo = [&](int u) { return smem + 2 * IMG + u * 2 * SLOT + SLOT; };
 
   const int g = blockIdx.x;
+  if (a.skew && (g & 1))
+    for (int k = 0; k < a.skew; ++k) __builtin_amdgcn_s_sleep(127);
   const long row0 = (long)g * R;
   const int C = a.C;
   const u16* ag = a.Ab + (long)g * C * V * V;
