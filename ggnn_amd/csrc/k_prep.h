@@ -297,9 +297,16 @@ __global__ void __launch_bounds__(256) k_stage_h0(const float* __restrict__ h0, 
     t[i][j4] = x.x; t[i][j4 + 1] = x.y; t[i][j4 + 2] = x.z; t[i][j4 + 3] = x.w;
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
-    const int j = q / 64, i = q % 64;
-    if (r0 + i < N) hT[wg_off(c0 + j, r0 + i, H)] = to_limb<F16>(t[i][j]);
+  // hT: 8 consecutive node rows of one hidden column are 16 contiguous bytes
+  // of the wg_off layout (N % 32 == 0, so a piece is all in or all out)
+  for (int q = threadIdx.x; q < 64 * 8; q += 256) {
+    const int j = q / 8, i = (q % 8) * 8;
+    if (r0 + i < N) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = pk<F16>(t[i + 2 * e][j], t[i + 2 * e + 1][j]);
+      *(uint4*)(hT + wg_off(c0 + j, r0 + i, H)) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
   }
 }
 
@@ -492,6 +499,15 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, lon
   const long stride = (long)gridDim.x * 256;
   long i = (long)blockIdx.x * 256 + threadIdx.x;
   if ((((unsigned long)x) & 15) == 0) {
+    // four independent 16-byte loads in flight per thread, then the rest
+    for (; 4 * (i + 3 * stride) + 3 < n; i += 4 * stride) {
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = *(const float4*)(x + 4 * (i + u * stride));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(a[u].x), fabsf(a[u].y)), fmaxf(fabsf(a[u].z), fabsf(a[u].w))));
+    }
     for (; 4 * i + 3 < n; i += stride) {
       const float4 a = *(const float4*)(x + 4 * i);
       m = fmaxf(m, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
