@@ -407,18 +407,48 @@ class DenseGGNNChemModel(BtbBatching):
         """Host LAS/UAS of the staged batch from the last build_loss() (the
         heads' probabilities are the only device tensors fetched).  Returns
         (las, uas, label_acc, labels, probs, mask, labels_e, probs_e, mask_e)."""
-        ph = self.placeholders
+        probs = self.ops["computed_values"].detach().cpu().numpy()
+        probs_e = self.ops["computed_values_edges"].detach().cpu().numpy()
+        return self._score_arrays(self.placeholders, probs, probs_e)
+
+    def _score_arrays(self, ph, probs, probs_e):
         b = int(ph["num_graphs"])
         v = int(ph["num_vertices"])
         o, oe = self.params["output_size"], self.output_size_edges
-        probs = self.ops["computed_values"].detach().cpu().numpy()
-        probs_e = self.ops["computed_values_edges"].detach().cpu().numpy()
         mask = np.asarray(ph["node_mask"], np.float32).reshape(b, v * o)
         mask_e = np.asarray(ph["node_mask_edges"], np.float32).reshape(b, v * oe)
         labels = np.asarray(ph["target_values_head"], np.float32).reshape(b, v * o)
         labels_e = np.asarray(ph["target_values_edges"], np.float32).reshape(b, v * oe)
         las, uas, uas_e = _eval.batch_las_uas(labels, probs, v, mask, labels_e, probs_e, mask_e, o, oe)
         return las, uas, uas_e, labels, probs, mask, labels_e, probs_e, mask_e
+
+    def _fetch_batch(self, loss, feed):
+        """Queue the device -> host copies of one batch's loss and heads'
+        probabilities (page-locked buffers, one event) and keep the host arrays
+        its scoring reads; _finish_batch waits for them.  run_epoch scores a
+        batch after queueing the next one, so the host's LAS/UAS work overlaps
+        the GPU step instead of alternating with it (the reference's sess.run
+        returns every fetch before the host continues, chem_tensorflow.py:594)."""
+        ph = dict(self.placeholders)
+        dev = [loss.detach(), self.ops["computed_values"].detach(), self.ops["computed_values_edges"].detach()]
+        p = {"b": int(feed["num_graphs"]), "feed": feed, "ph": ph}
+        if dev[0].device.type != "cuda":
+            p["host"], p["event"] = [t.cpu() for t in dev], None
+            return p
+        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in dev]
+        for h, t in zip(host, dev):
+            h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev[0].device))
+        p["host"], p["event"] = host, ev
+        return p
+
+    def _finish_batch(self, p):
+        """(loss, _score_arrays(...)) of a batch queued by _fetch_batch."""
+        if p["event"] is not None:
+            p["event"].synchronize()
+        hl, hp, hpe = p["host"]
+        return float(hl), self._score_arrays(p["ph"], hp.numpy(), hpe.numpy())
 
     # the reference's per-task "chemical accuracy" normalisers (chem_tensorflow.py:529-531)
     CHEMICAL_ACCURACIES = np.array([0.066513725, 0.012235489, 0.071939046, 0.033730778, 0.033486113, 0.004278493,
@@ -445,20 +475,14 @@ class DenseGGNNChemModel(BtbBatching):
         processed, steps = 0, 0
         acc_las = acc_uas = acc_uas_e = 0.0
         lists = {k: [] for k in ("labels", "cv", "nv", "mask", "ids", "adj", "labels_e", "cv_e", "mask_e")}
-        start = time.time()
-        for step, feed in enumerate(ThreadedIterator(self.make_minibatch_iterator(data, is_training),
-                                                     max_queue_size=5)):
-            b = int(feed["num_graphs"])
+
+        def consume(p):
+            # host side of one batch, run after the NEXT batch's step is queued
+            nonlocal loss, processed, steps, acc_las, acc_uas, acc_uas_e
+            b, feed = p["b"], p["feed"]
+            batch_loss, scored = self._finish_batch(p)
+            las, uas, uas_e, labels, cv, mask, labels_e, cv_e, mask_e = scored
             processed += b
-            if is_training:
-                feed["out_layer_dropout_keep_prob"] = self.params["out_layer_dropout_keep_prob"]
-                batch_loss = float(self.train_step(feed).detach())
-            else:
-                feed["out_layer_dropout_keep_prob"] = 1.0
-                self.feed(feed)
-                with torch.no_grad():
-                    batch_loss = float(self.build_loss())
-            las, uas, uas_e, labels, cv, mask, labels_e, cv_e, mask_e = self._score_batch()
             loss += batch_loss * b
             accuracies.append(np.array([batch_loss] * len(self.params["task_ids"])) * b)
             acc_las += las * b
@@ -466,12 +490,31 @@ class DenseGGNNChemModel(BtbBatching):
             acc_uas_e += uas_e * b
             if verbose:
                 print("Running %s, batch %i (has %i graphs). Loss so far: %.4f" % (
-                    epoch_name, step, b, loss / processed), end="\r")
+                    epoch_name, steps, b, loss / processed), end="\r")
             steps += 1
             for k, x in (("labels", labels), ("cv", cv), ("nv", int(feed["num_vertices"])), ("mask", mask),
                          ("ids", feed.get("sentences_id")), ("adj", feed.get("adjacency_matrix")),
                          ("labels_e", labels_e), ("cv_e", cv_e), ("mask_e", mask_e)):
                 lists[k].append(x)
+
+        start = time.time()
+        pending = None
+        for feed in ThreadedIterator(self.make_minibatch_iterator(data, is_training), max_queue_size=5):
+            if is_training:
+                feed["out_layer_dropout_keep_prob"] = self.params["out_layer_dropout_keep_prob"]
+                batch_loss = self.train_step(feed)
+            else:
+                feed["out_layer_dropout_keep_prob"] = 1.0
+                self.feed(feed)
+                with torch.no_grad():
+                    batch_loss = self.build_loss()
+            cur = self._fetch_batch(batch_loss, feed)
+            # one batch in flight: the host scores batch k while the GPU runs k + 1
+            if pending is not None:
+                consume(pending)
+            pending = cur
+        if pending is not None:
+            consume(pending)
         processed = max(processed, 1)
         accuracies = np.sum(accuracies, axis=0) / processed
         loss = loss / processed
