@@ -5,7 +5,7 @@
 //     m = b1 m + (1-b1) g'' ;  v = b2 v + (1-b2) g''^2
 //     p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps)
 // Two launches: per-tensor sums of squares (fp32 atomics into `sq`), then the
-// elementwise update.  HBM-bound: 4 reads + 3 writes of fp32 per element.
+// elementwise update.  HBM-bound: 4 reads + 3 writes of fp32 per element, as 16-byte pieces.
 #pragma once
 #include "ggnn_common.h"
 
@@ -32,7 +32,17 @@ __global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict
   const OptTensor& T = a.t[blockIdx.y];
   float acc = 0.f;
   if (!T.sqo) {
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < T.n; e += (long)gridDim.x * blockDim.x) {
+    const long st = (long)gridDim.x * blockDim.x;
+    long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((unsigned long)T.g) & 15) == 0) {  // 16-byte pieces, then the tail
+      for (; 4 * e + 3 < T.n; e += st) {
+        const float4 q = *(const float4*)(T.g + 4 * e);
+        const float x = a.gscale * q.x, y = a.gscale * q.y, z = a.gscale * q.z, w = a.gscale * q.w;
+        acc += (x * x + y * y) + (z * z + w * w);
+      }
+      e = (T.n & ~3L) + (long)blockIdx.x * blockDim.x + threadIdx.x;
+    }
+    for (; e < T.n; e += st) {
       const float g = a.gscale * T.g[e];
       acc += g * g;
     }
@@ -56,12 +66,35 @@ __global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __rest
   __syncthreads();
   // tf.clip_by_norm: t * clip / max(l2norm, clip)
   const float scale = a.gscale * a.clip / fmaxf(sqrtf(tot), a.clip);
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < T.n; e += (long)gridDim.x * blockDim.x) {
-    const float g = T.g[e] * scale;
-    const float m = a.b1 * T.m[e] + (1.0f - a.b1) * g;
-    const float v = a.b2 * T.v[e] + (1.0f - a.b2) * g * g;
+  auto upd = [&](float gg, float& m, float& v, float& p) {
+    const float g = gg * scale;
+    m = a.b1 * m + (1.0f - a.b1) * g;
+    v = a.b2 * v + (1.0f - a.b2) * g * g;
+    p -= a.lr_t * m / (sqrtf(v) + a.eps);
+  };
+  const long st = (long)gridDim.x * blockDim.x;
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // 16-byte pieces when all four arrays allow it (the same per-element
+  // arithmetic), then the tail
+  if (((((unsigned long)T.p) | ((unsigned long)T.g) | ((unsigned long)T.m) | ((unsigned long)T.v)) & 15) == 0) {
+    for (; 4 * e + 3 < T.n; e += st) {
+      const float4 g = *(const float4*)(T.g + 4 * e);
+      float4 m = *(const float4*)(T.m + 4 * e), v = *(const float4*)(T.v + 4 * e), p = *(const float4*)(T.p + 4 * e);
+      upd(g.x, m.x, v.x, p.x);
+      upd(g.y, m.y, v.y, p.y);
+      upd(g.z, m.z, v.z, p.z);
+      upd(g.w, m.w, v.w, p.w);
+      *(float4*)(T.m + 4 * e) = m;
+      *(float4*)(T.v + 4 * e) = v;
+      *(float4*)(T.p + 4 * e) = p;
+    }
+    e = (T.n & ~3L) + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  }
+  for (; e < T.n; e += st) {
+    float m = T.m[e], v = T.v[e], p = T.p[e];
+    upd(T.g[e], m, v, p);
     T.m[e] = m;
     T.v[e] = v;
-    T.p[e] -= a.lr_t * m / (sqrtf(v) + a.eps);
+    T.p[e] = p;
   }
 }
