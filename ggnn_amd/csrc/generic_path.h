@@ -426,7 +426,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       if (c.ed)
-        hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * H * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
+        hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * ((H + 3) / 4) * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
                            c.C, c.H, t, c.edrop);
     }
     // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)

@@ -88,23 +88,20 @@ __global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C,
   }
 }
 
-// ---- weights: fp32 copies, W masked per timestep under edge-weight dropout
-// (the fast path's Philox counter: (i>>2, j, c, t), word i&3)
-__global__ void k_gen_wmask(const float* __restrict__ W, float* __restrict__ out, int C, int H, int t, Drop dr) {
-  const long total = (long)C * H * H;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(e % H), i = (int)((e / H) % H), c = (int)(e / ((long)H * H));
-    float x = W[e];
-    if (dr.thr) x = drop_apply(dr, u4_get(edge_words(dr, c, i, j, t), i & 3), x);
-    out[e] = x;
-  }
-}
+// ---- edge-weight dropout (the fast path's Philox counter: (i>>2, j, c, t),
+// word i&3): one thread per (channel, row quad, column), the quad's 4 masks
+// being the words of one Philox block.
 // dW[c][i][j] += mask_t / keep * G[c][i][j]   (edge dropout backward, one timestep)
 __global__ void k_gen_wmask_acc(const float* __restrict__ G, float* __restrict__ dW, int C, int H, int t, Drop dr) {
-  const long total = (long)C * H * H;
+  const int HQ = (H + 3) / 4;
+  const long total = (long)C * HQ * H;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(e % H), i = (int)((e / H) % H), c = (int)(e / ((long)H * H));
-    dW[e] += drop_apply(dr, u4_get(edge_words(dr, c, i, j, t), i & 3), G[e]);
+    const int j = (int)(e % H), i0 = 4 * (int)((e / H) % HQ), c = (int)(e / ((long)HQ * H));
+    const uint4 w = edge_words(dr, c, i0, j, t);
+    for (int q = 0; q < 4 && i0 + q < H; ++q) {
+      const long o = ((long)c * H + i0 + q) * H + j;
+      dW[o] += drop_apply(dr, u4_get(w, q), G[o]);
+    }
   }
 }
 
