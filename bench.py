@@ -344,46 +344,69 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
     return res
 
 
-def end_to_end_side(dev, n_train=1000, n_valid=200, hidden=None, steps_note=""):
-    """Side measurement: the reference's own metric,
-    instance_per_sec of run_epoch (chem_tensorflow.py:528-667, :660) -- host
-    batching in a background thread, train step (front-end, propagation,
-    heads, clip + Adam) or eval forward, host LAS/UAS per batch -- with the
-    reference's default params (hidden_size 400, num_timesteps 4, batch_size
-    20, embeddings 80/50/100/80) on a synthetic treebank of WSJ-dev-like
-    sentence lengths (ggnn_amd.batching.synthetic_treebank; the treebank
-    itself is not distributed).  One warm-up epoch, then one timed train and
-    one timed valid epoch."""
-    from ggnn_amd.batching import synthetic_treebank
+def end_to_end_side(dev, rank=0, world=1, epochs=1, restrict=True):
+    """Side measurement (SURVEY §8f rank 4 / configs[0] / configs[4]): the
+    reference's own metric, instance_per_sec of run_epoch
+    (chem_tensorflow.py:528-667, :660) -- host batching in a background thread,
+    train step (front-end, propagation, heads, clip + Adam) or eval forward,
+    host LAS/UAS per batch -- with the reference's default params
+    (hidden_size 400, num_timesteps 4, batch_size 20, embeddings 80/50/100/80,
+    std -> nivre: C = 92 channels, 12 output labels) on the reference's OWN
+    sentences in its --train_with_dev mode (chem_tensorflow.py:36-45): train on
+    the 1700 std dev sentences, validate on the 2416 std test sentences
+    (data/, written from the reference's JSON; the train split is absent).
+    One warm-up epoch, then `epochs` timed train + valid epochs.  With
+    world > 1 every rank runs it: data-parallel run_epoch (rank-sharded
+    bucketed batches, one RCCL all-reduce of the whole model's flat gradient
+    buffer per global step), so the value is the N-rank job's instances/sec.
+    restrict: also the README's sample run (--restrict_data 100, epoch 1 of a
+    fresh model, train + valid; README.md:25-43)."""
+    from ggnn_amd.batching import TRAIN_WITH_DEV, wsj_model_sizes
     from ggnn_amd.model import DenseGGNNChemModel
-    raw = synthetic_treebank(n_train + n_valid, seed=2)
-    params = {"compact_adjacency": True}
-    if hidden:
-        params["hidden_size"] = hidden
-    m = DenseGGNNChemModel(num_edge_types=46, output_size_edges=12, pos_size=46, vocab_size=39549, params=params,
-                           seed=0, device=dev)
-    train = m.process_raw_graphs(raw[:n_train], True)
-    valid = m.process_raw_graphs(raw[n_train:], False)
+
+    def fresh():
+        np.random.seed(0)                      # chem_tensorflow.py:175
+        return DenseGGNNChemModel(params={"compact_adjacency": True}, seed=0, device=dev, rank=rank,
+                                  world_size=world, **wsj_model_sizes())
+
+    m = fresh()
+    t0 = time.perf_counter()
+    train = m.load_data(TRAIN_WITH_DEV["train_file"], True)
+    valid = m.load_data(TRAIN_WITH_DEV["valid_file"], False)
+    load_s = time.perf_counter() - t0
     m.run_epoch("warm-up", train, True)
-    tr = m.run_epoch("train", train, True)
-    va = m.run_epoch("valid", valid, False)
-    # README.md:25-43's sample run: --restrict_data 100 (100 sentences per
-    # split: small bucketed batches, avg 3.85 / 4.35 graphs), epoch 1
-    small = m.process_raw_graphs(raw[:100], True)
-    small_v = m.process_raw_graphs(raw[n_train:n_train + 100], False)
-    tr100 = m.run_epoch("train r100", small, True)
-    va100 = m.run_epoch("valid r100", small_v, False)
-    return {"params": {k: m.params[k] for k in ("hidden_size", "num_timesteps", "batch_size")},
-            "train_instances_per_sec": tr[3], "train_steps": tr[4], "train_loss": tr[0],
-            "valid_instances_per_sec": va[3], "valid_las": va[5], "valid_uas": va[6],
-            "sentences": {"train": n_train, "valid": n_valid},
-            "restrict_data_100": {"train_instances_per_sec": tr100[3], "train_steps": tr100[4],
-                                  "avg_train_batch": 100 / max(tr100[4], 1),
-                                  "valid_instances_per_sec": va100[3], "valid_steps": va100[4],
-                                  "reference_readme": {"train_instances_per_sec": 13.91,
-                                                       "valid_instances_per_sec": 31.51,
-                                                       "hardware": "unstated (BASELINE.md §1)"}},
-            "note": "the reference's run_epoch metric (host batching + LAS/UAS included), not the hot-path value"}
+    res = {"params": {k: m.params[k] for k in ("hidden_size", "num_timesteps", "batch_size")},
+           "data": "WSJ std->nivre btb, --train_with_dev: train = std dev (1700 sentences), valid = std test (2416)",
+           "n_ranks": world, "load_and_process_s": load_s, "epochs": []}
+    for e in range(epochs):
+        tr = m.run_epoch("train", train, True)
+        va = m.run_epoch("valid", valid, False)
+        res["epochs"].append({"train_instances_per_sec": tr[3], "train_steps": tr[4], "train_loss": tr[0],
+                              "train_las": tr[5], "train_uas": tr[6], "train_uas_e": tr[16],
+                              "valid_instances_per_sec": va[3], "valid_loss": va[0], "valid_las": va[5],
+                              "valid_uas": va[6], "valid_uas_e": va[16]})
+    res.update({k: res["epochs"][-1][k] for k in ("train_instances_per_sec", "valid_instances_per_sec",
+                                                   "valid_las", "valid_uas")})
+    if restrict:
+        # README.md:25-43's sample run: --restrict_data 100 (100 sentences per
+        # split: small bucketed batches), epoch 1 of a fresh model (cold: the
+        # first batch of every bucket shape allocates its workspace)
+        m2 = fresh()
+        small = m2.load_data(TRAIN_WITH_DEV["train_file"], True, restrict=100)
+        small_v = m2.load_data(TRAIN_WITH_DEV["valid_file"], False, restrict=100)
+        tr100 = m2.run_epoch("train r100", small, True)
+        va100 = m2.run_epoch("valid r100", small_v, False)
+        res["restrict_data_100_epoch1"] = {
+            "train_instances_per_sec": tr100[3], "train_steps": tr100[4], "avg_train_batch": 100 / max(tr100[4], 1),
+            "train_las_uas_uas_e": [tr100[5], tr100[6], tr100[16]],
+            "valid_instances_per_sec": va100[3], "valid_las_uas_uas_e": [va100[5], va100[6], va100[16]],
+            "reference_readme": {"train_instances_per_sec": 13.91, "valid_instances_per_sec": 31.51,
+                                 "train_las_uas_uas_e": [0.106, 0.147, 0.576],
+                                 "valid_las_uas_uas_e": [0.191, 0.232, 0.750],
+                                 "hardware": "unstated (BASELINE.md §1)"}}
+    res["note"] = ("the reference's run_epoch metric (host batching + LAS/UAS included), not the hot-path value; "
+                   "dropout as the reference feeds it in training (0.9 / 0.55 / 0.85), none in validation")
+    return res
 
 
 def load_ceilings():
@@ -566,12 +589,14 @@ def main():
     breakdown = {k: {"ms_per_step": timer.total_ms[k] / args.steps, "launches_per_step": timer.launches[k] / args.steps}
                  for k in kinds}
 
+    # the reference's own end-to-end run_epoch on its sentences: every rank
+    # (data-parallel when world > 1), before the rank-0-only side lines
+    e2e = end_to_end_side(dev, rank, world, restrict=(world == 1)) if not args.no_side else None
     feed_cmp = adjacency_feed_costs(eng, b, v, CFG["e"], dev) if rank == 0 else None
     callers = callers_side(dev, b, v, h) if rank == 0 and not args.no_side else None
     bf16 = (precision_side(dev, "bf16", A_d, h0_d, w_d, dhT, b, v, h, C, T)
             if rank == 0 and not args.no_side and args.precision != "bf16" else None)
     real = real_density_side(dev) if rank == 0 and not args.no_side else None
-    e2e = end_to_end_side(dev) if rank == 0 and not args.no_side else None
 
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]

@@ -24,9 +24,42 @@ reference's order so seeded training batches coincide.
 """
 from __future__ import annotations
 
+import json
+import lzma
+import os
 from collections import defaultdict
 
 import numpy as np
+
+# the reference's WSJ btb treebank files (std dev / test JSON, xz-compressed)
+# and their label / POS lists, written by tests/golden/make_golden.py
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+# --train_with_dev (chem_tensorflow.py:36-45, std input bank): train on the std
+# dev set, validate on the std test set (the train split is absent)
+TRAIN_WITH_DEV = {"train_file": "wsj_std_dev_btb.json.xz", "valid_file": "wsj_std_test_btb.json.xz"}
+
+
+def read_btb_json(path):
+    """A btb treebank JSON (parser/to_graph.py's output), plain or .xz."""
+    opener = lzma.open if path.endswith(".xz") else open
+    with opener(path, "rt") as f:
+        return json.load(f)
+
+
+def wsj_model_sizes(data_dir=None):
+    """The vocabulary-derived sizes of the reference's std -> nivre btb model
+    (chem_tensorflow.py:183-199): num_edge_types = len(dep_list) + 1,
+    output_size_edges = len(dep_list_out), pos_size = len(pos_list) (at least
+    1 + the largest POS index of the JSON: the absent train CoNLL holds tags
+    the dev / test files lack), vocab_size, max_nodes and bucket_max_nodes
+    (the first bucket above max_nodes, :191-193)."""
+    with open(os.path.join(data_dir or DATA_DIR, "wsj_vocab.json")) as f:
+        voc = json.load(f)
+    buckets = np.array(list(range(4, 200, 2)))
+    return {"num_edge_types": len(voc["dep_list_std"]) + 1, "output_size_edges": len(voc["dep_list_nivre"]),
+            "pos_size": max(len(voc["pos_list_std"]), 46), "vocab_size": int(voc["vocab_size"]),
+            "max_nodes": int(voc["max_nodes"]),
+            "bucket_max_nodes": int(buckets[np.argmax(buckets > int(voc["max_nodes"]))])}
 
 
 def graph_to_adj_mat_bd(graph, max_n_vertices, num_edge_types):
@@ -173,6 +206,17 @@ class BtbBatching:
                                  chosen_bucket_size, self.params.get("tie_fwd_bkwd", True))
 
     # ------------------------------------------------------------- datasets
+    def load_data(self, file_name, is_training_data, data_dir=None, restrict=None, skip=None):
+        """chem_tensorflow.py:241-269: read a btb JSON from data_dir (default:
+        the repo's data/), drop the first ``skip`` graphs (--skip_data), keep
+        the first ``restrict`` (--restrict_data), then process_raw_graphs."""
+        data = read_btb_json(os.path.join(data_dir or DATA_DIR, file_name))
+        if skip is not None and int(skip) > 0:
+            data = data[int(skip):]
+        if restrict is not None and int(restrict) > 0:
+            data = data[:int(restrict)]
+        return self.process_raw_graphs(data, is_training_data)
+
     def process_raw_graphs(self, raw_data, is_training_data, bucket_sizes=None):
         """Bucket graphs by max node id, densify adjacency per graph.
         Returns (bucketed, bucket_sizes, bucket_at_step)."""
@@ -259,8 +303,11 @@ class BtbBatching:
         out[:, :, :v] = lab.sum(axis=1)                # sum over e, pad v -> o
         return out.reshape(b, v * o)
 
-    def make_minibatch_iterator(self, data, is_training):
-        """Yields feed dicts keyed by placeholder name (chem_tensorflow_dense.py:792-875)."""
+    def minibatch_schedule(self, data, is_training):
+        """The batches of one epoch as (bucket index, elements) in the order the
+        reference yields them (chem_tensorflow_dense.py:792-875): the shuffles
+        (bucket_at_step, then every bucket, on the global numpy RNG) happen
+        before the first batch, as at the top of the reference's generator."""
         bucketed, bucket_sizes, bucket_at_step = data
         if is_training:
             np.random.shuffle(bucket_at_step)
@@ -268,34 +315,76 @@ class BtbBatching:
                 np.random.shuffle(bd)
         counters = defaultdict(int)
         bs = self.params["batch_size"]
+        out = []
+        for bidx in bucket_at_step:
+            out.append((bidx, bucketed[bidx][counters[bidx] * bs:(counters[bidx] + 1) * bs]))
+            counters[bidx] += 1
+        return out
+
+    def target_count(self, elements, task_id=0):
+        """sum(target_mask[task]) of a batch of these elements: make_batch's
+        task mask is 0 for a label set to None by task_sample_ratios, else 1
+        (chem_tensorflow_dense.py:757-767, chem_tensorflow.py:358-360)."""
+        internal = self.params["task_ids"].index(task_id)
+        return float(sum(0.0 if d["labels"][internal] is None else 1.0 for d in elements))
+
+    def make_minibatch_iterator(self, data, is_training, rank=0, world_size=1):
+        """Yields feed dicts keyed by placeholder name (chem_tensorflow_dense.py:792-875).
+
+        Data parallel (world_size > 1): every rank computes the same schedule
+        (the same seeded shuffles) and global step k takes its batches
+        k*N .. k*N+N-1, batch k*N+r going to rank r, so N consecutive batches
+        of the single-process order run at once.  Each feed carries
+        ``global_target_count`` / ``global_num_graphs`` of its global step
+        (train_step's loss normaliser; no communication needed).  A rank
+        without a batch in the last global step gets a feed with
+        num_graphs == 0 (it still joins the step's all-reduce)."""
+        sched = self.minibatch_schedule(data, is_training)
+        bucket_sizes = data[1]
+        if world_size <= 1:
+            for bidx, elements in sched:
+                yield self._make_feed(elements, int(bucket_sizes[bidx]), is_training)
+            return
+        if not 0 <= rank < world_size:
+            raise ValueError("rank %d outside world_size %d" % (rank, world_size))
+        for k in range(0, len(sched), world_size):
+            group = sched[k:k + world_size]
+            count = sum(self.target_count(el) for _, el in group)
+            graphs = sum(len(el) for _, el in group)
+            if rank < len(group):
+                bidx, elements = group[rank]
+                feed = self._make_feed(elements, int(bucket_sizes[bidx]), is_training)
+            else:
+                feed = {"num_graphs": 0}
+            feed["global_target_count"] = count
+            feed["global_num_graphs"] = graphs
+            yield feed
+
+    def _make_feed(self, elements, v, is_training):
         keep = self.params.get("graph_state_dropout_keep_prob", 1.0) if is_training else 1.0
         emb_keep = self.params.get("emb_dropout_keep_prob", 1.0) if is_training else 1.0
         # the output-layer keep is fed 1.0 outside training (run_epoch, chem_tensorflow.py:586-592)
         out_keep = self.params.get("out_layer_dropout_keep_prob", 1.0) if is_training else 1.0
-        for bidx in bucket_at_step:
-            elements = bucketed[bidx][counters[bidx] * bs:(counters[bidx] + 1) * bs]
-            batch = self.make_batch(elements)
-            b, v = len(batch["init"]), int(bucket_sizes[bidx])
-            pad = lambda key: self.get_word_inputs_padded(batch[key], b, v)
-            word_inputs = np.stack((pad("words_loc"), pad("words_pos"), pad("words_index"),
-                                    pad("words_head"), pad("words_head_pos"), pad("edges_index")), axis=2)
-            feed = {
-                "target_values_head": self.get_target_values_formatted(batch["labels"]),
-                "target_values_edges": self.get_target_values_edges_formatted(batch["labels"]),
-                "target_mask": np.transpose(batch["task_masks"], axes=[1, 0]),
-                "num_graphs": b,
-                "num_vertices": v,
-                "adjacency_matrix": None if batch["adj_mat"][0] is None else batch["adj_mat"],
-                "adjacency_edges": batch["graph"],
-                "node_mask": np.array(batch["node_mask"]),
-                "node_mask_edges": np.array(batch["node_mask_edges"]),
-                "graph_state_keep_prob": keep,
-                "edge_weight_dropout_keep_prob": keep,
-                "emb_dropout_keep_prob": emb_keep,
-                "out_layer_dropout_keep_prob": out_keep,
-                "sentences_id": batch["sentences_id"],
-                "word_inputs": word_inputs,
-                "target_pos": pad("target_pos"),
-            }
-            counters[bidx] += 1
-            yield feed
+        batch = self.make_batch(elements)
+        b = len(batch["init"])
+        pad = lambda key: self.get_word_inputs_padded(batch[key], b, v)
+        word_inputs = np.stack((pad("words_loc"), pad("words_pos"), pad("words_index"),
+                                pad("words_head"), pad("words_head_pos"), pad("edges_index")), axis=2)
+        return {
+            "target_values_head": self.get_target_values_formatted(batch["labels"]),
+            "target_values_edges": self.get_target_values_edges_formatted(batch["labels"]),
+            "target_mask": np.transpose(batch["task_masks"], axes=[1, 0]),
+            "num_graphs": b,
+            "num_vertices": v,
+            "adjacency_matrix": None if batch["adj_mat"][0] is None else batch["adj_mat"],
+            "adjacency_edges": batch["graph"],
+            "node_mask": np.array(batch["node_mask"]),
+            "node_mask_edges": np.array(batch["node_mask_edges"]),
+            "graph_state_keep_prob": keep,
+            "edge_weight_dropout_keep_prob": keep,
+            "emb_dropout_keep_prob": emb_keep,
+            "out_layer_dropout_keep_prob": out_keep,
+            "sentences_id": batch["sentences_id"],
+            "word_inputs": word_inputs,
+            "target_pos": pad("target_pos"),
+        }

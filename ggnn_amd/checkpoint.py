@@ -104,17 +104,29 @@ def save_progress(model, model_path: str, train_step: int, valid_step: int) -> N
         pickle.dump(data, f, pickle.HIGHEST_PROTOCOL)
 
 
-def _adam_step_count(data, opt):
+def _adam_step_count(data, opt, log=print):
     """Adam's step count t: the stored integer, else recovered from the
     float32 beta powers (beta2 ** t stays a normal float32 far longer than
-    beta1 ** t, which underflows near t = 1000); None if absent."""
+    beta1 ** t, which underflows near t = 1000); None if absent.
+
+    The recovery is approximate: TF keeps the powers as a float32 running
+    product, which drifts by a few steps at large t, and beta2 ** t itself
+    leaves the normal float32 range near t = 87k (beyond that nothing can be
+    recovered and Adam's bias correction restarts from t = 0).  Both cases
+    are logged."""
     if "adam_step" in data:
         return int(data["adam_step"])
     saved = data["weights"]
     for key, beta in (("beta2_power:0", opt.b2), ("beta1_power:0", opt.b1)):
         p = float(saved.get(key, 0.0))
         if 0.0 < p < 1.0 and p >= 1.1754944e-38:
-            return int(round(math.log(p) / math.log(beta)))
+            t = int(round(math.log(p) / math.log(beta)))
+            log("Adam step count recovered as %d from the float32 %s (approximate: no integer adam_step "
+                "in this checkpoint)." % (t, key))
+            return t
+    if any(k in saved for k in ("beta1_power:0", "beta2_power:0")):
+        log("Adam step count could not be recovered from the saved beta powers (float32 range exceeded); "
+            "Adam's bias correction restarts from step 0.")
     return None
 
 
@@ -146,7 +158,7 @@ def restore_progress(model, model_path: str, log=print):
             elif n in names:
                 log("Freshly initializing %s since no saved value was found." % n)
     if opt is not None:
-        t = _adam_step_count(data, opt)
+        t = _adam_step_count(data, opt, log)
         if t is not None:
             opt.t = t
         used.update(n for n in ("beta1_power:0", "beta2_power:0") if n in saved)

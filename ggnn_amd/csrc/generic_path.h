@@ -120,8 +120,9 @@ static bool ring_ok(const GemmArgs& a, bool A16, bool AKC, bool BKC) {
   }
   return true;
 }
-// ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail)
-static int g_gemm_force = 0;
+// ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail);
+// thread-local, so a forward / backward on another thread never sees it
+static thread_local int g_gemm_force = 0;
 // GGNN_GEMM_KERNEL=old forces k_gemm everywhere (A/B measurements)
 static int gemm_kernel_env() {
   static const int v = [] {

@@ -792,7 +792,8 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
     if (a.count == PACK_MAXJ) flush();
     PackJob& J = a.j[a.count];
-    if (mode == 2 && drop) n /= 4;  // (one thread per 4-row quad, k_pack_multi)
+    // (one thread per 4-row quad of a column, k_pack_multi; a partial last quad when H % 4 != 0)
+    if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
     J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop;
     a.blk_begin[a.count++] = nb;
     nb += (int)((n + 255) / 256);
@@ -1106,6 +1107,12 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
   for (int i = 0; i < nseg; ++i) {
     if (!segs[i].d_table) return fail(GGNN_EINVAL, "embed_backward: NULL d_table");
     gd.dtable[i] = segs[i].d_table;
+    // a table looked up by several segments has ONE gradient (the reference's
+    // IndexedSlices concatenate both lookups' rows): its squared norm goes to
+    // the slot of the first segment with that d_table
+    gd.sqslot[i] = i;
+    for (int j = 0; j < i; ++j)
+      if (segs[j].d_table == segs[i].d_table) { gd.sqslot[i] = j; break; }
   }
   Prof p(K_HEADS, s);
   {

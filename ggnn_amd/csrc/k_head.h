@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(256) k_embed_fwd(EmbArgs a, const int* __restr
 // One thread per (row quad, column), as k_embed_fwd.
 struct EmbGrad {
   float* dtable[EMB_MAXSEG];
+  int sqslot[EMB_MAXSEG];  // lookup_sqnorm slot of each segment: the first segment with the same d_table
 };
 __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const int* __restrict__ wi,
                                                    const float* __restrict__ dh0, const float* __restrict__ dh0_add,
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
   __syncthreads();
   if (threadIdx.x < a.nseg) {
     const int i = threadIdx.x;
-    atomicAdd(sq + i, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+    atomicAdd(sq + gd.sqslot[i], red[0][i] + red[1][i] + red[2][i] + red[3][i]);
   }
 }
 

@@ -433,13 +433,15 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
       ((float*)J.out)[q] = J.S[q];
       return;
     }
-    // masked: one thread per 4-row quad of one column (J.total = C*H*H / 4),
+    // masked: one thread per 4-row quad of one column (J.total = C*HQ*H,
+    // HQ = ceil(H/4): the last quad of a W_c is partial when H % 4 != 0),
     // whose 4 masks are the 4 words of one Philox block
-    const int H = J.K, hq = H >> 2;
+    const int H = J.K, hq = (H + 3) >> 2;
     const int wj = (int)(q % H), iq = (int)((q / H) % hq), c = (int)(q / ((long)H * hq));
     const uint4 w = edge_words(a.dr, c, 4 * iq, wj, J.t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
+      if (4 * iq + u >= H) break;
       const long e = ((long)c * H + 4 * iq + u) * H + wj;
       ((float*)J.out)[e] = drop_apply(a.dr, u4_get(w, u), J.S[e]);
     }

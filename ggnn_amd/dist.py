@@ -1,5 +1,10 @@
 """Data-parallel plumbing: one process per GPU, gradients all-reduced over RCCL.
 
+Two flat buffers: ``FlatGradients`` (the path's six weight gradients, the
+propagation-only step of bench.py) and ``FlatTrainBuffer`` (every trainable
+variable of the btb model plus the IndexedSlices norms and the losses, the
+whole training step of ``DenseGGNNChemModel.train_step``).
+
 The propagation path shards naturally by graph (chem_tensorflow_dense.py:414-428
 contracts only inside graph g); the only cross-graph coupling is the batch sum
 of the weight gradients (TF autodiff, chem_tensorflow.py:496).  Each rank runs
@@ -63,6 +68,50 @@ class FlatGradients:
         """Sum the gradients over all ranks (RCCL on GPUs, gloo on CPU)."""
         if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size(group) > 1:
             tdist.all_reduce(self.flat, op=tdist.ReduceOp.SUM, group=group)
+
+
+class FlatTrainBuffer:
+    """ONE contiguous fp32 buffer for a whole btb training step of the model
+    (``DenseGGNNChemModel.train_step``): the gradient of every trainable
+    variable (the path's six tensors, the loc/pos/word embedding tables and
+    both output heads' W, b), then the tables' squared lookup norms (the
+    IndexedSlices norms ``tf.clip_by_norm`` takes, chem_tensorflow.py:498-500)
+    and the per-head losses.  Every producer writes straight into its views
+    (ggnn_backward, ggnn_heads_backward, ggnn_embed_backward, heads forward),
+    so a data-parallel step is a single all-reduce of ``flat`` with no packing
+    copy, and it sums the gradients, the lookup norms and the losses at once.
+
+    Each view starts on a 64-float (256-byte) boundary (the library's
+    16-byte vector paths and the MFMA epilogues' stores)."""
+
+    ALIGN = 64
+
+    def __init__(self, params, n_sq: int, n_loss: int, device=None):
+        sizes = [int(p.numel()) for p in params] + [int(n_sq), int(n_loss)]
+        offs, off = [], 0
+        for n in sizes:
+            offs.append(off)
+            off += -(-n // self.ALIGN) * self.ALIGN
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grads = [self.flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
+        self.sq = self.flat[offs[-2]:offs[-2] + n_sq]
+        self.loss = self.flat[offs[-1]:offs[-1] + n_loss]
+
+    @property
+    def nbytes(self) -> int:
+        return self.flat.numel() * 4
+
+    def zero_(self) -> None:
+        """A rank without a batch in this global step contributes zeros."""
+        self.flat.zero_()
+
+
+def all_reduce_sum(group=None):
+    """A callable summing a tensor over the ranks of `group` (RCCL on GPUs,
+    gloo on CPU), or None outside a multi-rank job."""
+    if not (tdist.is_available() and tdist.is_initialized() and tdist.get_world_size(group) > 1):
+        return None
+    return lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
 
 
 def init_from_env(backend: str | None = None):

@@ -94,14 +94,16 @@ class EmbeddingFrontEnd:
                    "ggnn_embed_forward")
         return h0
 
-    def backward(self, segments, wi, dh0, keep=1.0, seed=0, dh0_add=None, dtables=None):
-        """Returns (per-segment dense table gradients, per-segment lookup sqnorm
-        device scalars).  dtables: optional per-segment gradient buffers;
+    def backward(self, segments, wi, dh0, keep=1.0, seed=0, dh0_add=None, dtables=None, sq_out=None):
+        """Returns (per-segment dense table gradients, lookup sqnorm device
+        vector [nseg]).  dtables: optional per-segment gradient buffers;
         segments that share a table may share one buffer (the kernel adds both
-        segments' lookups into it)."""
+        segments' lookups into it, and the table's squared lookup norm goes to
+        the first such segment's slot).  sq_out: optional [nseg] fp32 output
+        (e.g. a view into a flat all-reduce buffer)."""
         b, v, ncols = wi.shape
         dts = dtables if dtables is not None else [torch.empty_like(t) for t, _ in segments]
-        sq = torch.empty(len(segments), dtype=torch.float32, device=wi.device)
+        sq = sq_out if sq_out is not None else torch.empty(len(segments), dtype=torch.float32, device=wi.device)
         d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32")
         _lib.check(self._lib.ggnn_embed_backward(ctypes.byref(d), self._segs(segments, dts), len(segments), _ptr(wi),
                                                  ncols, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
@@ -130,11 +132,13 @@ class OutputHeads:
                                 None if dbs is None else dbs[i].data_ptr())
         return arr
 
-    def forward(self, hT, h0, heads, labels=None, keep=1.0, seed=0, target_num=1.0):
-        """Returns (probs list [b, v, o], loss tensor [nheads] or None)."""
+    def forward(self, hT, h0, heads, labels=None, keep=1.0, seed=0, target_num=1.0, loss_out=None, probs_out=None):
+        """Returns (probs list [b, v, o], loss tensor [nheads] or None).
+        loss_out / probs_out: optional output buffers (loss [nheads] fp32)."""
         b, v, h = hT.shape
         dev = hT.device
-        probs = [torch.empty(b, v, W.shape[1], dtype=torch.float32, device=dev) for W, _ in heads]
+        probs = probs_out if probs_out is not None else [torch.empty(b, v, W.shape[1], dtype=torch.float32, device=dev)
+                                                          for W, _ in heads]
         d = _lib.dims(b, v, h, 1, 1, True, "fp32")
         tab = self._table(heads, labels, probs)
         n = ctypes.c_size_t(0)
@@ -142,7 +146,9 @@ class OutputHeads:
                    "ggnn_heads_workspace_bytes")
         if self._ws is None or self._ws.numel() < n.value:
             self._ws = torch.empty(max(int(n.value), 1), dtype=torch.uint8, device=dev)
-        loss = torch.empty(len(heads), dtype=torch.float32, device=dev) if labels is not None else None
+        loss = None
+        if labels is not None:
+            loss = loss_out if loss_out is not None else torch.empty(len(heads), dtype=torch.float32, device=dev)
         _lib.check(self._lib.ggnn_heads_forward(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
                                                 _ptr(h0.contiguous()), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                 float(target_num), _ptr(loss), _ptr(self._ws), _stream()),
@@ -150,16 +156,18 @@ class OutputHeads:
         self._saved = (b, v, h)
         return probs, loss
 
-    def backward(self, hT, h0, heads, labels, probs, target_num=1.0, d_loss=None):
+    def backward(self, hT, h0, heads, labels, probs, target_num=1.0, d_loss=None, dws=None, dbs=None, dhT=None,
+                 dh0=None):
         """Gradients of sum(loss) (times d_loss, a device scalar): dW, db per
-        head and (dhT, dh0).  Uses the workspace of the last forward."""
+        head and (dhT, dh0).  Uses the workspace of the last forward.  dws, dbs,
+        dhT, dh0: optional output buffers (overwritten)."""
         b, v, h = hT.shape
         if self._saved != (b, v, h):
             raise RuntimeError("heads backward without a matching forward")
-        dws = [torch.empty_like(W) for W, _ in heads]
-        dbs = [torch.empty_like(bb) for _, bb in heads]
-        dhT = torch.empty_like(hT)
-        dh0 = torch.empty_like(h0)
+        dws = dws if dws is not None else [torch.empty_like(W) for W, _ in heads]
+        dbs = dbs if dbs is not None else [torch.empty_like(bb) for _, bb in heads]
+        dhT = dhT if dhT is not None else torch.empty_like(hT)
+        dh0 = dh0 if dh0 is not None else torch.empty_like(h0)
         d = _lib.dims(b, v, h, 1, 1, True, "fp32")
         _lib.check(self._lib.ggnn_heads_backward(ctypes.byref(d), self._table(heads, labels, probs, dws, dbs),
                                                  len(heads), _ptr(hT.contiguous()), _ptr(h0.contiguous()),
@@ -192,10 +200,8 @@ class EmbedFunction(torch.autograd.Function):
             if first[i] == i:
                 bufs[i] = torch.empty_like(t)
         dts, sq = ctx.fe.backward(segs, ctx.wi, dh0, ctx.keep, ctx.seed, dtables=[bufs[f] for f in first])
-        norms = {}
-        for i, t in enumerate(ctx.tables):
-            norms[id(t)] = sq[i:i + 1] if id(t) not in norms else norms[id(t)] + sq[i:i + 1]
-        ctx.owner.lookup_sqnorm = norms
+        # (a table's squared lookup norm is in its first segment's slot)
+        ctx.owner.lookup_sqnorm = {id(t): sq[first[i]:first[i] + 1] for i, t in enumerate(ctx.tables)}
         out = tuple(bufs[i] if first[i] == i else None for i in range(len(ctx.tables)))
         return (None, None, None, None, None, None) + out
 

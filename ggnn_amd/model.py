@@ -36,8 +36,10 @@ import numpy as np
 import torch
 
 from . import checkpoint as _ckpt
+from . import dist as _dist
 from . import evaluation as _eval
 from .batching import BtbBatching, ThreadedIterator
+from .dist import FlatTrainBuffer
 from .engine import PropagationEngine
 from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
 from .optim import ClipAdam
@@ -96,8 +98,15 @@ class DenseGGNNChemModel(BtbBatching):
 
     def __init__(self, args=None, params=None, num_edge_types=None, output_size_edges=12, pos_size=46,
                  bucket_max_nodes=120, device=None, seed=None, precision="fp32", vocab_size=1000, max_nodes=None,
-                 embedding_sizes=None):
+                 embedding_sizes=None, rank=0, world_size=1, group=None):
+        """rank, world_size, group: data-parallel training (one process per GPU,
+        ``torch.distributed`` initialised by the caller, e.g. dist.init_from_env):
+        run_epoch then draws this rank's share of every global step's batches
+        and train_step sums the flat gradient buffer over the group (RCCL)."""
         self.args = dict(args or {"--pr": "btb"})
+        self.rank, self.world_size, self.group = int(rank), int(world_size), group
+        if not 0 <= self.rank < self.world_size:
+            raise ValueError("rank %d outside world_size %d" % (self.rank, self.world_size))
         self.params = self.default_params()
         if params:
             self.params.update(params)
@@ -183,8 +192,17 @@ class DenseGGNNChemModel(BtbBatching):
                                                 "biases": [t(np.zeros([shape[1]], np.float32))]}
         self._front_end = None
         self._heads = None
+        self._flat = None
         self.lookup_sqnorm = {}
         self.optimizer = None
+
+    def _seed(self) -> int:
+        """A fresh 64-bit Philox seed from the model's RandomState (a new mask
+        per step, like TF's stateful RNG).  Rank r of a data-parallel job XORs
+        a rank constant in, so the ranks' masks are independent (rank 0, and a
+        single process, keep the plain draw)."""
+        s = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        return s ^ ((self.rank * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)
 
     def parameters(self):
         ps = [self.weights["edge_weights"], self.weights["edge_weights_fixed"]]
@@ -267,24 +285,36 @@ class DenseGGNNChemModel(BtbBatching):
             h0 = torch.from_numpy(np.ascontiguousarray(np.asarray(h0, dtype=np.float32)))
         h0 = h0.to(device=self.device, dtype=torch.float32)
         eng = self._engine("main" if fixed_ts is None else "fixed")
-        if self.placeholders["adjacency_matrix"] is not None:
-            eng.set_adjacency(self.placeholders["adjacency_matrix"])
-        else:
-            eng.set_adjacency_edges(self.placeholders["adjacency_edges"], int(self.placeholders["num_vertices"]),
-                                    self.num_edge_types)
+        self._stage_adjacency(eng)
         gru = self.weights["node_gru"]
         # dropout as fed (chem_tensorflow_dense.py:860-861 training, :938-940 eval);
         # a fresh Philox seed per call = fresh masks per step, like TF's stateful RNG
-        edge_keep = float(self.placeholders.get("edge_weight_dropout_keep_prob", 1.0))
-        state_keep = float(self.placeholders.get("graph_state_keep_prob", 1.0))
-        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        edge_keep, state_keep = self._path_keeps()
+        seed = self._seed()
         out = _Propagate.apply(h0, W, beta, gru["gates_kernel"], gru["gates_bias"],
                                gru["candidate_kernel"], gru["candidate_bias"], eng, T, edge_keep, state_keep, seed)
         self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=seed)
         self.ops["final_node_representations" if fixed_ts is None else "second_node_representations"] = out
         return out
 
+    def _stage_adjacency(self, eng) -> None:
+        if self.placeholders["adjacency_matrix"] is not None:
+            eng.set_adjacency(self.placeholders["adjacency_matrix"])
+        else:
+            eng.set_adjacency_edges(self.placeholders["adjacency_edges"], int(self.placeholders["num_vertices"]),
+                                    self.num_edge_types)
+
+    def _path_keeps(self):
+        """(edge_weight_dropout_keep_prob, graph_state_keep_prob) as fed."""
+        return (float(self.placeholders.get("edge_weight_dropout_keep_prob", 1.0)),
+                float(self.placeholders.get("graph_state_keep_prob", 1.0)))
+
     # ------------------------------------------------- §8f rank 1: callers
+    def _front_end_segments(self):
+        """(tables, word_inputs columns) of the btb front-end in concat order."""
+        W = self.weights
+        return (W["loc_embeddings"], W["pos_embeddings"], W["word_embeddings"], W["loc_embeddings"]), (0, 1, 2, 3)
+
     def get_initial_node_representation(self):
         """btb front-end (chem_tensorflow_dense.py:264-306): lookups of
         word_inputs columns 0 (loc), 1 (pos), 2 (word), 3 (head loc, the loc
@@ -298,13 +328,11 @@ class DenseGGNNChemModel(BtbBatching):
         if width > h:
             raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
                              "(SURVEY F7); pass smaller embedding_sizes" % (width, h))
-        W = self.weights
-        tables = (W["loc_embeddings"], W["pos_embeddings"], W["word_embeddings"], W["loc_embeddings"])
-        cols = (0, 1, 2, 3)
+        tables, cols = self._front_end_segments()
         wi = word_inputs_tensor(self.placeholders["word_inputs"], self.device,
                                 {c: tb.shape[0] for tb, c in zip(tables, cols)})
         keep = float(self.placeholders.get("emb_dropout_keep_prob", 1.0))
-        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        seed = self._seed()
         if self._front_end is None:
             self._front_end = EmbeddingFrontEnd(h)
         h0 = EmbedFunction.apply(self._front_end, self, wi, keep, seed, cols, *tables)
@@ -320,19 +348,10 @@ class DenseGGNNChemModel(BtbBatching):
         hT = self.compute_final_node_representations(h0)
         b, v, h = hT.shape
         o, oe = self.params["output_size"], self.output_size_edges
-        if v > o:
-            raise ValueError("num_vertices %d > output_size %d" % (v, o))
-        y_h = self._up_labels(np.asarray(self.placeholders["target_values_head"], np.float32).reshape(b, v, o),
-                              self.device)
-        y_e = self._up_labels_e(np.asarray(self.placeholders["target_values_edges"], np.float32).reshape(b, v, oe),
-                                self.device)
-        labels = [y_h, y_e]
-        tmask = np.asarray(self.placeholders["target_mask"], np.float64)
-        internal = self.params["task_ids"].index(task_id)
-        target_num = float(tmask[internal].sum() + SMALL_NUMBER)
-        keep = float(self.placeholders.get("out_layer_dropout_keep_prob",
-                                           self.params["out_layer_dropout_keep_prob"]))
-        seed = int(self._rng.randint(0, 2 ** 31 - 1)) << 32 | int(self._rng.randint(0, 2 ** 31 - 1))
+        labels = self._head_labels(b, v)
+        target_num = float(self._target_count(task_id) + SMALL_NUMBER)
+        keep = self._out_keep()
+        seed = self._seed()
         if self._heads is None:
             self._heads = OutputHeads(h)
         g = self.weights["regression_gate_task%i" % task_id]
@@ -345,26 +364,163 @@ class DenseGGNNChemModel(BtbBatching):
         self.last_heads = dict(keep=keep, seed=seed, target_num=target_num)
         return loss
 
-    def train_step(self, feed_dict=None, grad_scale=1.0, all_reduce=None):
+    def _head_labels(self, b, v):
+        """The two heads' targets [b, v, o] / [b, v, e_o] on the device
+        (placeholders target_values_head / _edges, chem_tensorflow.py:372-376)."""
+        o, oe = self.params["output_size"], self.output_size_edges
+        if v > o:
+            raise ValueError("num_vertices %d > output_size %d" % (v, o))
+        y_h = self._up_labels(np.asarray(self.placeholders["target_values_head"], np.float32).reshape(b, v, o),
+                              self.device)
+        y_e = self._up_labels_e(np.asarray(self.placeholders["target_values_edges"], np.float32).reshape(b, v, oe),
+                                self.device)
+        return [y_h, y_e]
+
+    def _target_count(self, task_id=0) -> float:
+        """sum(target_mask[task]) of the staged batch (chem_tensorflow.py:358-360)."""
+        tmask = np.asarray(self.placeholders["target_mask"], np.float64)
+        return float(tmask[self.params["task_ids"].index(task_id)].sum())
+
+    def _out_keep(self) -> float:
+        return float(self.placeholders.get("out_layer_dropout_keep_prob", self.params["out_layer_dropout_keep_prob"]))
+
+    def _heads_list(self, task_id=0):
+        g = self.weights["regression_gate_task%i" % task_id]
+        ge = self.weights["regression_gate_task_edges%i" % task_id]
+        return [(g["weights"][0], g["biases"][0]), (ge["weights"][0], ge["biases"][0])]
+
+    def train_buffer(self) -> FlatTrainBuffer:
+        """The flat gradient / lookup-norm / loss buffer of train_step."""
+        if self._flat is None:
+            self._flat = FlatTrainBuffer(self.trainable_variables(), n_sq=4, n_loss=2, device=self.device)
+        return self._flat
+
+    def train_step(self, feed_dict=None, grad_scale=1.0, all_reduce=None, target_count=None, task_id=0):
         """One training step (chem_tensorflow.py:483-506 + run_epoch's
-        sess.run of train_step): loss, backward, per-variable clip_by_norm,
-        Adam.  all_reduce: optional callable on the list of gradients (data
-        parallel; pass grad_scale = 1/N).  Returns the loss tensor."""
+        sess.run of train_step): front-end -> propagation -> heads -> loss,
+        the backward of each, per-variable clip_by_norm, Adam.  Returns the
+        loss (a device scalar).
+
+        Every gradient lands in ONE flat fp32 buffer (``train_buffer()``: all
+        trainable variables, the embedding tables' IndexedSlices norms and the
+        per-head losses), written in place by the library's backward calls.
+
+        Data parallel (``all_reduce``: a callable summing a tensor over the
+        ranks; run_epoch passes it when world_size > 1): the loss of a global
+        step is the reference's btb loss (chem_tensorflow.py:358-360,399-403)
+        over the UNION of the ranks' batches, i.e. every rank normalises its
+        cross-entropy by the global ``target_count`` (sum of target_mask over
+        all ranks' graphs; the feed's ``global_target_count`` from the sharded
+        iterator) + SMALL_NUMBER.  Then the per-rank gradients, lookup norms
+        (sum of squared rows of the concatenated IndexedSlices) and losses
+        simply add: one all-reduce of the flat buffer, and clip + Adam on the
+        sums with grad_scale 1.  With dropout off this equals one process
+        stepping the concatenated batch.  A feed with num_graphs == 0 (a rank
+        without a batch in the last global step) contributes zeros."""
+        if feed_dict is not None and int(feed_dict.get("num_graphs", 1)) == 0:
+            return self._empty_train_step(all_reduce, grad_scale)
         if feed_dict is not None:
             self.feed(feed_dict)
+        if target_count is None:
+            target_count = self.placeholders.get("global_target_count")
+        fl = self.train_buffer()
         params = self.trainable_variables()
-        for p in params:
-            p.grad = None
-        loss = self.build_loss()
-        loss.backward()
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+        self._forward_backward(fl, params, None if target_count is None else float(target_count), task_id)
         if all_reduce is not None:
-            all_reduce(grads)
+            all_reduce(fl.flat)
+        self._apply_gradients(fl, params, grad_scale)
+        return fl.loss.sum()
+
+    def _empty_train_step(self, all_reduce, grad_scale):
+        fl = self.train_buffer()
+        fl.zero_()
+        if all_reduce is not None:
+            all_reduce(fl.flat)
+        self._apply_gradients(fl, self.trainable_variables(), grad_scale)
+        return fl.loss.sum()
+
+    def _apply_gradients(self, fl, params, grad_scale):
         if self.optimizer is None:
             self.make_optimizer()
+        tables = self._front_end_segments()[0]
+        # the tables' squared lookup norms (first segment's slot per table)
+        slot = {}
+        for i, t in enumerate(tables):
+            slot.setdefault(id(t), i)
+        self.lookup_sqnorm = {k: fl.sq[i:i + 1] for k, i in slot.items()}
         sq = [self.lookup_sqnorm.get(id(p)) for p in params]
-        self.optimizer.step(grads, grad_scale=grad_scale, sqnorms=sq)
-        return loss
+        for p, g in zip(params, fl.grads):
+            p.grad = g
+        self.optimizer.step(fl.grads, grad_scale=grad_scale, sqnorms=sq)
+
+    def _forward_backward(self, fl, params, target_count, task_id):
+        """The btb loss and every gradient of one staged batch, written into
+        the flat buffer ``fl`` (no autograd: each backward of the library
+        writes its outputs where the optimizer reads them).  The dropout seeds
+        are drawn in build_loss's order (front-end, path, heads)."""
+        if "word_inputs" not in self.placeholders:
+            raise RuntimeError("feed() a minibatch with word_inputs first")
+        if self.args.get("--pr", "btb") != "btb":
+            raise NotImplementedError("only --pr btb is supported by the engine")
+        h = self.params["hidden_size"]
+        gv = {id(p): g for p, g in zip(params, fl.grads)}
+        # front-end (chem_tensorflow_dense.py:264-306)
+        tables, cols = self._front_end_segments()
+        width = self.loc_embedding_size * 2 + self.pos_embedding_size + self.word_embedding_size
+        if width > h:
+            raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
+                             "(SURVEY F7); pass smaller embedding_sizes" % (width, h))
+        wi = word_inputs_tensor(self.placeholders["word_inputs"], self.device,
+                                {c: tb.shape[0] for tb, c in zip(tables, cols)})
+        keep_e = float(self.placeholders.get("emb_dropout_keep_prob", 1.0))
+        seed_e = self._seed()
+        if self._front_end is None:
+            self._front_end = EmbeddingFrontEnd(h)
+        segs = list(zip(tables, cols))
+        h0 = self._front_end.forward(segs, wi, keep_e, seed_e)
+        self.last_embed = dict(keep=keep_e, seed=seed_e)
+        self.ops["initial_node_representations"] = h0
+        # propagation (chem_tensorflow_dense.py:312-340)
+        T = self.params["num_timesteps"]
+        eng = self._engine("main")
+        self._stage_adjacency(eng)
+        edge_keep, state_keep = self._path_keeps()
+        seed_p = self._seed()
+        W, gru = self.weights, self.weights["node_gru"]
+        beta = W["edge_biases"] if self.params["use_edge_bias"] else None
+        wts = {"edge_weights": W["edge_weights"], "edge_biases": beta, "gates_kernel": gru["gates_kernel"],
+               "gates_bias": gru["gates_bias"], "candidate_kernel": gru["candidate_kernel"],
+               "candidate_bias": gru["candidate_bias"]}
+        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=seed_p)
+        hT = eng.forward(h0, pack, T, training=True, state_keep=state_keep)
+        self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=seed_p)
+        self.ops["final_node_representations"] = hT
+        # heads + btb loss (chem_tensorflow_dense.py:439-516, chem_tensorflow.py:326-421)
+        b, v, _ = hT.shape
+        o, oe = self.params["output_size"], self.output_size_edges
+        labels = self._head_labels(b, v)
+        count = self._target_count(task_id) if target_count is None else target_count
+        target_num = float(count + SMALL_NUMBER)
+        keep_o = self._out_keep()
+        seed_o = self._seed()
+        if self._heads is None:
+            self._heads = OutputHeads(h)
+        hl = self._heads_list(task_id)
+        probs, _ = self._heads.forward(hT, h0, hl, labels, keep_o, seed_o, target_num, loss_out=fl.loss)
+        self.last_heads = dict(keep=keep_o, seed=seed_o, target_num=target_num)
+        self.ops["computed_values"] = probs[0].reshape(b, v * o)
+        self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
+        _, _, dhT, dh0_heads = self._heads.backward(hT, h0, hl, labels, probs, target_num,
+                                                     dws=[gv[id(w)] for w, _ in hl], dbs=[gv[id(bb)] for _, bb in hl])
+        # the path's backward (TF autodiff, chem_tensorflow.py:496)
+        eg = {"h0": torch.empty_like(h0), "edge_weights": gv[id(W["edge_weights"])],
+              "edge_biases": gv[id(beta)] if beta is not None else None,
+              "gates_kernel": gv[id(gru["gates_kernel"])], "gates_bias": gv[id(gru["gates_bias"])],
+              "candidate_kernel": gv[id(gru["candidate_kernel"])], "candidate_bias": gv[id(gru["candidate_bias"])]}
+        eng.backward(dhT, eg)
+        # the tables' gradients + IndexedSlices norms (h0 feeds the path and the heads)
+        self._front_end.backward(segs, wi, eg["h0"], keep_e, seed_e, dh0_add=dh0_heads,
+                                 dtables=[gv[id(t)] for t in tables], sq_out=fl.sq)
 
     def make_optimizer(self) -> ClipAdam:
         """The reference's train step optimizer (chem_tensorflow.py:494-503) over
@@ -469,7 +625,16 @@ class DenseGGNNChemModel(BtbBatching):
         Fetch diet: the reference's sess.run fetches 21 tensors per batch,
         among them the dense [b, 2E, v, v] adjacency, the final node states and
         the whole word-embedding table (:560-593); here only the loss and the
-        two heads' probabilities leave the device."""
+        two heads' probabilities leave the device.
+
+        Data parallel (world_size > 1): each rank runs its share of every
+        global step (make_minibatch_iterator(rank, world_size)); a training
+        step all-reduces the flat gradient buffer once (train_step).  The loss,
+        LAS/UAS sums and graph counts are summed over the ranks once at the
+        end of the epoch, and instance_per_sec is all ranks' graphs over the
+        slowest rank's epoch time; a training batch's loss is the global
+        step's (union-batch) loss.  The per-batch lists (labels, computed
+        values, ...) hold this rank's batches only."""
         loss = 0.0
         accuracies = []
         processed, steps = 0, 0
@@ -499,10 +664,19 @@ class DenseGGNNChemModel(BtbBatching):
 
         start = time.time()
         pending = None
-        for feed in ThreadedIterator(self.make_minibatch_iterator(data, is_training), max_queue_size=5):
+        world = self.world_size
+        all_reduce = _dist.all_reduce_sum(self.group) if world > 1 else None
+        if world > 1 and all_reduce is None:
+            raise RuntimeError("world_size %d but torch.distributed is not initialised" % world)
+        it = self.make_minibatch_iterator(data, is_training, rank=self.rank, world_size=world)
+        for feed in ThreadedIterator(it, max_queue_size=5):
+            if int(feed["num_graphs"]) == 0:     # no batch for this rank in the last global step
+                if is_training:
+                    self.train_step(feed, all_reduce=all_reduce)
+                continue
             if is_training:
                 feed["out_layer_dropout_keep_prob"] = self.params["out_layer_dropout_keep_prob"]
-                batch_loss = self.train_step(feed)
+                batch_loss = self.train_step(feed, all_reduce=all_reduce)
             else:
                 feed["out_layer_dropout_keep_prob"] = 1.0
                 self.feed(feed)
@@ -515,11 +689,25 @@ class DenseGGNNChemModel(BtbBatching):
             pending = cur
         if pending is not None:
             consume(pending)
+        elapsed = time.time() - start
+        acc_sum = np.sum(accuracies, axis=0) if accuracies else np.zeros(len(self.params["task_ids"]))
+        if world > 1:
+            # one reduction of the epoch's sums over the ranks (off the step loop)
+            dev = self.device if torch.distributed.get_backend(self.group) == "nccl" else torch.device("cpu")
+            tot = torch.tensor([processed, loss, acc_las, acc_uas, acc_uas_e, steps] + list(acc_sum),
+                               dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(tot, group=self.group)
+            mx = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX, group=self.group)
+            t = tot.cpu().numpy()
+            processed, loss, acc_las, acc_uas, acc_uas_e, steps = (float(t[0]), float(t[1]), float(t[2]), float(t[3]),
+                                                                   float(t[4]), int(t[5]))
+            acc_sum, elapsed = t[6:], float(mx.item())
         processed = max(processed, 1)
-        accuracies = np.sum(accuracies, axis=0) / processed
+        accuracies = acc_sum / processed
         loss = loss / processed
         error_ratios = accuracies / self.CHEMICAL_ACCURACIES[self.params["task_ids"]]
-        instance_per_sec = processed / (time.time() - start)
+        instance_per_sec = processed / elapsed
         return (loss, accuracies, error_ratios, instance_per_sec, steps, acc_las / processed, acc_uas / processed,
                 lists["labels"], lists["cv"], lists["nv"], lists["mask"], lists["ids"], lists["adj"], lists["labels_e"],
                 lists["cv_e"], lists["mask_e"], acc_uas_e / processed)

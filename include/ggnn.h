@@ -125,8 +125,11 @@ int ggnn_workspace_bytes(const ggnn_dims* d, int training, size_t* bytes);
 int ggnn_adjacency_bytes(const ggnn_dims* d, size_t* bytes);
 int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes);
 
-/* Convert fp32 master weights into the engine's bf16 MFMA fragment layouts.
- * edge_biases may be NULL when !(flags & GGNN_USE_EDGE_BIAS). */
+/* Convert fp32 master weights into the engine's MFMA fragment layouts, in the
+ * precision policy of d->flags: bf16 (flag 0), f16 (GGNN_FP16) or an f16
+ * hi/lo limb pair per element (GGNN_FP32_PARITY); plus the fp32 bias copies
+ * and the general path's fp32 weight copies (one per timestep under edge
+ * dropout, masked).  edge_biases may be NULL when !(flags & GGNN_USE_EDGE_BIAS). */
 int ggnn_pack_weights(const ggnn_dims* d, void* pack,
                       const float* edge_weights, const float* edge_biases,
                       const float* gates_kernel, const float* gates_bias,
@@ -242,8 +245,13 @@ int ggnn_embed_forward(const ggnn_dims* d, const ggnn_embed_segment* segs, int n
                        float* h0, ggnn_stream_t stream);
 /* Gradients of the tables from dL/dh0 (+ dh0_add when not NULL: the two uses
  * of h0, the propagation input and the heads' concat), same keep and seed as
- * the forward.  lookup_sqnorm: device float[nseg], per segment the sum of
- * squares of its per-lookup gradient rows (overwritten). */
+ * the forward.  lookup_sqnorm: device float[nseg] (overwritten), per TABLE the
+ * sum of squares of its per-lookup gradient rows, i.e. the squared norm
+ * tf.clip_by_norm takes of the reference's IndexedSlices gradient
+ * (chem_tensorflow.py:498-500).  Segments sharing a d_table (btb: the loc
+ * table, looked up by word_inputs columns 0 and 3) have ONE gradient whose
+ * rows are both lookups' rows: their sum goes to the slot of the first such
+ * segment, the later segments' slots are 0. */
 int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg,
                         const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
                         const float* dh0, const float* dh0_add, float* lookup_sqnorm,

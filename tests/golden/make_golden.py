@@ -3,11 +3,25 @@ helpers (run here, in the build container; /root/reference is not on the GPU
 box).  TensorFlow and docopt are absent from the image, so
 they are stubbed in sys.modules -- only the reference's numpy code runs:
 graph_to_adj_mat_bd, process_raw_graphs and make_minibatch_iterator of
-chem_tensorflow_dense.py.  Output: tests/golden/batching_golden.npz.
+chem_tensorflow_dense.py.  Outputs:
+
+* tests/golden/batching_golden.npz -- adjacency / feed / batch-order fixtures;
+* tests/golden/eval_golden.npz -- the host LAS/UAS scoring of the reference's
+  own adj_mat_to_target, get_las_uas and humanize_batch_results_btb
+  (chem_tensorflow_dense.py:106-131, 1160-1215, 1304-1319) on real dev batches
+  with seeded random head / label probabilities (quantised to uint8 levels so
+  the fixture stores them exactly);
+* data/wsj_std_{dev,test}_btb.json.xz -- the reference's std dev / test btb
+  treebank JSON (data, xz-compressed) and data/wsj_vocab.json -- the label /
+  POS lists of get_dep_and_pos_list (parser/to_graph.py:206-255) from the
+  dev + test CoNLL (the train CoNLL is absent) and the vocabulary
+  size from the JSON's word indices: the inputs of the --train_with_dev run
+  (chem_tensorflow.py:36-45) on the GPU box, where /root/reference is absent.
 
     python tests/golden/make_golden.py
 """
 import json
+import lzma
 import os
 import sys
 import types
@@ -15,7 +29,10 @@ import types
 import numpy as np
 
 REF = "/root/reference"
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "batching_golden.npz")
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "batching_golden.npz")
+EVAL_OUT = os.path.join(HERE, "eval_golden.npz")
+DATA = os.path.join(os.path.dirname(os.path.dirname(HERE)), "data")
 
 
 def stub_modules():
@@ -107,6 +124,80 @@ def main():
                                                 fd["graph_state_keep_prob"], fd["emb_dropout_keep_prob"]])
     np.savez_compressed(OUT, **out)
     print("wrote %s (%d eval batches, %d train batches)" % (OUT, len(feeds), len(tfeeds)))
+    eval_fixtures(ref, m, data, feeds)
+    data_fixtures(dep_in, dep_out, pos_list, max_nodes)
+
+
+def eval_fixtures(ref, m, data, feeds):
+    """LAS/UAS of the reference's own scoring functions on real dev batches."""
+    m.args = {"--pr": "btb"}
+    o, oe = m.params["output_size"], m.output_size_edges
+    rng = np.random.default_rng(2024)
+    out = {"output_size": o, "output_size_edges": oe, "num_edge_types": m.num_edge_types}
+    nb = 0
+    for bi, fd in enumerate(feeds[:6]):
+        b, v = int(fd["num_graphs"]), int(fd["num_vertices"])
+        labels = np.asarray(fd["target_values_head"])
+        labels_e = np.asarray(fd["target_values_edges"])
+        # probabilities: uint8 levels / 255 (ties when the levels are few);
+        # half of the batches get the target boosted so LAS/UAS are not ~0
+        levels = 255 if bi % 2 == 0 else 7
+        ph = rng.integers(0, levels + 1, labels.shape).astype(np.uint8)
+        pe = rng.integers(0, levels + 1, labels_e.shape).astype(np.uint8)
+        if bi % 3 != 2:
+            boost = rng.random(labels.shape) < 0.6
+            ph = np.where((labels > 0) & boost, np.uint8(levels), ph)
+            boost_e = rng.random(labels_e.shape) < 0.6
+            pe = np.where((labels_e > 0) & boost_e, np.uint8(levels), pe)
+        cv = ph.astype(np.float32) / np.float32(levels)
+        cv_e = pe.astype(np.float32) / np.float32(levels)
+        mask, mask_e = np.asarray(fd["node_mask"]), np.asarray(fd["node_mask_edges"])
+        adms = np.asarray(fd["adjacency_matrix"])
+        las, uas, uas_e = m.humanize_batch_results_btb(
+            labels=labels, computed_values=cv, num_vertices=v, mask=mask, ids=fd["sentences_id"], adms=adms,
+            labels_e=labels_e, computed_values_e=cv_e, mask_edges=mask_e)
+        # per graph: the reference's target / result graphs
+        _, res, tgt = m.get_results_reshaped(targets=labels, computed_values=cv, mask=mask, num_vertices=v)
+        _, res_e, tgt_e = m.get_results_reshaped(targets=labels_e, computed_values=cv_e, mask=mask_e,
+                                                 num_vertices=v, is_edge=True)
+        graphs = []
+        for i in range(b):
+            tg = m.merge_head_and_edge_graph(ref.adj_mat_to_target(tgt[i]), ref.adj_mat_to_target(tgt_e[i]))
+            rg_h = ref.adj_mat_to_target(res[i], is_probability=True)
+            rg_e = ref.adj_mat_to_target(res_e[i], is_probability=True)
+            rg = m.merge_head_and_edge_graph(rg_h, rg_e)
+            l1, u1 = m.get_las_uas(tg, rg)
+            graphs.append(dict(target=tg, result=rg, result_e=rg_e, las=l1, uas=u1))
+        pre = "b%d_" % bi
+        out[pre + "levels"] = levels
+        out[pre + "probs_head"] = ph
+        out[pre + "probs_edges"] = pe
+        out[pre + "batch"] = bi
+        out[pre + "las_uas_uase"] = np.array([las, uas, uas_e], np.float64)
+        out[pre + "graphs"] = np.array(json.dumps(graphs, default=int))
+        nb += 1
+    out["n_batches"] = nb
+    np.savez_compressed(EVAL_OUT, **out)
+    print("wrote %s (%d batches)" % (EVAL_OUT, nb))
+
+
+def data_fixtures(dep_in, dep_out, pos_list, max_nodes):
+    os.makedirs(DATA, exist_ok=True)
+    words = 0
+    for src, dst in (("en-wsj-std-dev-stanford-3.3.0-tagged_btb.json", "wsj_std_dev_btb.json.xz"),
+                     ("en-wsj-std-test-stanford-3.3.0-tagged_btb.json", "wsj_std_test_btb.json.xz")):
+        with open(os.path.join(REF, src), "rb") as f:
+            raw = f.read()
+        words = max(words, max(max(d["words_index"]) for d in json.loads(raw)))
+        with lzma.open(os.path.join(DATA, dst), "wb", preset=9) as f:
+            f.write(raw)
+    vocab = {"source": "parser/to_graph.py:206-255 get_dep_and_pos_list over the std / nivre dev + test CoNLL "
+                       "(train CoNLL absent); vocab_size = 1 + max words_index of the std dev + test JSON",
+             "dep_list_std": dep_in, "dep_list_nivre": dep_out, "pos_list_std": pos_list, "max_nodes": max_nodes,
+             "vocab_size": words + 1}
+    with open(os.path.join(DATA, "wsj_vocab.json"), "w") as f:
+        json.dump(vocab, f, indent=1)
+    print("wrote %s" % DATA)
 
 
 if __name__ == "__main__":

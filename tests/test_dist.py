@@ -71,3 +71,143 @@ def test_flat_gradient_layout():
     assert float(fg.flat.sum()) == 3.0 * 32
     fg2 = FlatGradients(16, 6, False)
     assert "edge_biases" not in fg2.views
+
+
+# ---------------------------------------------------------------------------
+# The data-parallel btb training loop (run_epoch / train_step with
+# world_size > 1): rank-sharded bucketed batches and the union-batch loss.
+
+def _golden_model(batch_size=6, hidden=48):
+    import json
+    from ggnn_amd.model import DenseGGNNChemModel
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "batching_golden.npz"))
+    data = json.loads(str(g["raw_json"]))
+    vocab = 1 + max(max(d["words_index"]) for d in data)
+    m = DenseGGNNChemModel(params={"hidden_size": hidden, "num_timesteps": 2, "batch_size": batch_size},
+                           num_edge_types=int(g["num_edge_types"]), output_size_edges=int(g["output_size_edges"]),
+                           pos_size=int(g["pos_size"]), bucket_max_nodes=int(g["bucket_max_nodes"]), device="cpu",
+                           vocab_size=vocab, embedding_sizes=dict(loc=8, pos=4, word=8, edge=4))
+    return m, data
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+@pytest.mark.parametrize("training", [True, False])
+def test_rank_sharded_iterator_partitions_the_schedule(world, training):
+    """Every rank runs the same seeded schedule and takes batch k*N + r of
+    global step k: together the ranks see exactly the single-process batches
+    (chem_tensorflow_dense.py:792-875), each global step's feeds carry its
+    total target count, and ranks past the last batch get empty feeds."""
+    m, data = _golden_model()
+
+    def feeds(rank, w):
+        np.random.seed(0)       # chem_tensorflow.py:175
+        return list(m.make_minibatch_iterator(m.process_raw_graphs(data, training), training, rank=rank,
+                                              world_size=w))
+
+    single = feeds(0, 1)
+    per_rank = [feeds(r, world) for r in range(world)]
+    steps = -(-len(single) // world)
+    assert all(len(f) == steps for f in per_rank)
+    for k in range(steps):
+        group = single[k * world:(k + 1) * world]
+        count = sum(float(np.asarray(f["target_mask"])[0].sum()) for f in group)
+        for r in range(world):
+            f = per_rank[r][k]
+            assert f["global_target_count"] == count and f["global_num_graphs"] == sum(x["num_graphs"] for x in group)
+            if r < len(group):
+                ref = group[r]
+                assert list(f["sentences_id"]) == list(ref["sentences_id"])
+                assert f["num_vertices"] == ref["num_vertices"]
+                np.testing.assert_array_equal(f["word_inputs"], ref["word_inputs"])
+                np.testing.assert_array_equal(f["adjacency_matrix"], ref["adjacency_matrix"])
+            else:
+                assert f["num_graphs"] == 0
+
+
+def _btb_weights(m, seed):
+    rng = np.random.default_rng(seed)
+    h, C = m.params["hidden_size"], m.num_channels
+    o, oe = m.params["output_size"], m.output_size_edges
+    u = lambda *s: rng.uniform(-0.3, 0.3, s)
+    return {"loc_embeddings": u(m.max_nodes, 8), "pos_embeddings": u(m.pos_size, 4),
+            "word_embeddings": u(m.vocab_size, 8), "edge_weights": u(C, h, h) * 0.5, "edge_biases": u(C, 1, h) * 0.1,
+            "gates_kernel": u(2 * h, 2 * h), "gates_bias": 1.0 + u(2 * h) * 0.1, "candidate_kernel": u(2 * h, h),
+            "candidate_bias": u(h) * 0.1, "head_W": u(2 * h, o), "head_b": u(o) * 0.1, "edge_W": u(2 * h, oe),
+            "edge_b": u(oe) * 0.1}
+
+
+_BTB_ORDER = ("edge_weights", "edge_biases", "gates_kernel", "gates_bias", "candidate_kernel", "candidate_bias",
+              "loc_embeddings", "pos_embeddings", "word_embeddings", "head_W", "head_b", "edge_W", "edge_b")
+
+
+def _union_feeds(m, data):
+    """Two batches of one bucket (A, B) and their concatenation A+B."""
+    proc = m.process_raw_graphs(data, False)
+    bucketed, sizes, _ = proc
+    bidx = max(bucketed, key=lambda k: len(bucketed[k]))
+    els = bucketed[bidx]
+    n = len(els) // 2
+    v = int(sizes[bidx])
+    return m._make_feed(els[:n], v, False), m._make_feed(els[n:2 * n], v, False), m._make_feed(els[:2 * n], v, False)
+
+
+def _union_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from ggnn_amd.dist import init_from_env
+    import torch.distributed as tdist
+    init_from_env(backend="gloo")
+    m, data = _golden_model(hidden=32)
+    fa, fb, fab = _union_feeds(m, data)
+    P = _btb_weights(m, 3)
+    h, T, o, oe = m.params["hidden_size"], 2, m.params["output_size"], m.output_size_edges
+    # every rank normalises by the GLOBAL target count (train_step's rule)
+    count = float(np.asarray(fa["target_mask"])[0].sum() + np.asarray(fb["target_mask"])[0].sum())
+    mine = (fa, fb)[rank]
+    loss, g, sq = O.btb_loss_and_grads(P, mine, h, T, o, oe, count + O.SMALL_NUMBER)
+    flat = torch.from_numpy(np.concatenate([g[k].ravel() for k in _BTB_ORDER] +
+                                           [np.array([sq["loc_embeddings"], sq["pos_embeddings"],
+                                                      sq["word_embeddings"], loss])]))
+    tdist.all_reduce(flat)
+    if rank == 0:
+        l_u, g_u, sq_u = O.btb_loss_and_grads(P, fab, h, T, o, oe, count + O.SMALL_NUMBER)
+        ref = np.concatenate([g_u[k].ravel() for k in _BTB_ORDER] +
+                             [np.array([sq_u["loc_embeddings"], sq_u["pos_embeddings"], sq_u["word_embeddings"],
+                                        l_u])])
+        q.put(float(np.abs(flat.numpy() - ref).max() / np.abs(ref).max()))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_two_rank_btb_step_equals_union_batch():
+    """The DP rule of train_step on the float64 oracle, two gloo ranks: each
+    rank's btb loss over its own batch, normalised by the global target count
+    (chem_tensorflow.py:358-360,399-403), then ONE sum of [every variable's
+    gradient | the tables' IndexedSlices squared norms | the loss] equals the
+    reference's step over the concatenated batch -- gradients, the clip norms
+    tf.clip_by_norm sees (chem_tensorflow.py:498-500) and the loss."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_union_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    err = q.get(timeout=5)
+    assert err < 1e-12, err
+
+
+def test_flat_train_buffer_layout():
+    from ggnn_amd.dist import FlatTrainBuffer
+    ps = [torch.zeros(3, 5), torch.zeros(7), torch.zeros(2, 2, 2)]
+    fb = FlatTrainBuffer(ps, n_sq=4, n_loss=2)
+    assert [tuple(g.shape) for g in fb.grads] == [(3, 5), (7,), (2, 2, 2)]
+    assert all(g.data_ptr() % 256 == fb.flat.data_ptr() % 256 for g in fb.grads)
+    fb.grads[1].fill_(1.0)
+    fb.sq.fill_(2.0)
+    fb.loss.fill_(3.0)
+    assert float(fb.flat.sum()) == 7.0 + 8.0 + 6.0
+    fb.zero_()
+    assert float(fb.flat.abs().sum()) == 0.0

@@ -188,3 +188,37 @@ def test_adj_mat_to_target_vectorised_matches_loop():
             a[0, min(1, nv - 1), 0] = np.nan
         for p in (False, True):
             assert E.adj_mat_to_target(a, p) == _adj_mat_to_target_loop(a, p), (trial, p)
+
+
+def test_las_uas_equal_the_reference_on_real_dev_batches():
+    """Host LAS/UAS (evaluation.py) against fixtures written by the
+    reference's OWN adj_mat_to_target, get_las_uas and
+    humanize_batch_results_btb (chem_tensorflow_dense.py:106-131, 1160-1215,
+    1304-1319; tests/golden/make_golden.py) on real WSJ dev batches with
+    seeded head / label probabilities (ties included): bit-exact, per batch
+    and per graph."""
+    import json
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    ev = np.load(os.path.join(here, "eval_golden.npz"))
+    g = np.load(os.path.join(here, "batching_golden.npz"))
+    o, oe = int(ev["output_size"]), int(ev["output_size_edges"])
+    for k in range(int(ev["n_batches"])):
+        pre = "b%d_" % k
+        bi = int(ev[pre + "batch"])
+        b, v = (int(x) for x in g["eval%d_scalars" % bi][:2])
+        lv = np.float32(int(ev[pre + "levels"]))
+        cv = ev[pre + "probs_head"].astype(np.float32) / lv
+        cv_e = ev[pre + "probs_edges"].astype(np.float32) / lv
+        labels, labels_e = g["eval%d_target_values_head" % bi], g["eval%d_target_values_edges" % bi]
+        mask, mask_e = g["eval%d_node_mask" % bi], g["eval%d_node_mask_edges" % bi]
+        got = E.batch_las_uas(labels, cv, v, mask, labels_e, cv_e, mask_e, o, oe)
+        assert tuple(got) == tuple(ev[pre + "las_uas_uase"]), (k, got, ev[pre + "las_uas_uase"])
+        _, res, tgt = E.results_reshaped_btb(labels, cv, mask, v, o, oe)
+        _, res_e, tgt_e = E.results_reshaped_btb(labels_e, cv_e, mask_e, v, o, oe, is_edge=True)
+        for i, ref in enumerate(json.loads(str(ev[pre + "graphs"]))):
+            tg = E.merge_head_and_edge_graph(E.adj_mat_to_target(tgt[i]), E.adj_mat_to_target(tgt_e[i]))
+            rg_e = E.adj_mat_to_target(res_e[i], is_probability=True)
+            rg = E.merge_head_and_edge_graph(E.adj_mat_to_target(res[i], is_probability=True), rg_e)
+            assert tg == ref["target"] and rg == ref["result"] and rg_e == ref["result_e"], (k, i)
+            assert E.get_las_uas(tg, rg) == (ref["las"], ref["uas"])
+    assert int(ev["n_batches"]) >= 6

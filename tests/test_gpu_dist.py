@@ -62,6 +62,45 @@ def test_two_rank_engine_step_equals_full_batch(tmp_path, shape):
     assert np.abs(step_dp - step_full).max() <= 1e-3 * np.abs(step_full).max()
 
 
+def _spawn(script, args, tmp_path):
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", script)] + args, env=env,
+                                      cwd=ROOT))
+    codes = [p.wait(timeout=300) for p in procs]
+    assert codes == [0, 0], codes
+
+
+@pytest.mark.parametrize("hidden", [128, 400])
+def test_two_rank_btb_train_step_equals_union_batch(tmp_path, hidden):
+    """The data-parallel training step of the WHOLE btb model (front-end,
+    propagation, heads, clip + Adam; hidden 128 = specialised kernels, 400 =
+    the general path): two ranks, each on one of two real dev batches of one
+    bucket, one all-reduce of the flat buffer per step, equal one process
+    stepping the concatenated batch -- the reference's loss over the union
+    (chem_tensorflow.py:358-360,399-403) -- after two train_steps."""
+    out = str(tmp_path / "dp_train.npz")
+    _spawn("dist_train_worker.py", [out, str(hidden)], tmp_path)
+    d = np.load(out)
+    for s in range(2):
+        ref = d["full_flat"][s]
+        err = np.abs(d["dp_flat"][s] - ref).max() / np.abs(ref).max()
+        assert err <= 1e-4, (s, err)                      # gradients, lookup norms, losses
+    np.testing.assert_allclose(d["dp_loss"], d["full_loss"], rtol=1e-5)
+    step_full = d["full_params"] - d["init"]
+    assert np.abs(step_full).max() > 1e-4
+    assert np.abs(d["dp_params"] - d["full_params"]).max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
+    # run_epoch with world_size 2: every batch of the single-process schedule
+    # ran once (steps summed over the ranks), finite loss, LAS/UAS fractions
+    tr_loss, tr_ips, tr_steps, tr_las, tr_uas, va_loss, va_ips, va_steps, va_las, va_uas, n_tr, n_va = d["epoch"]
+    assert tr_steps == n_tr and va_steps == n_va
+    assert np.isfinite(tr_loss) and np.isfinite(va_loss) and tr_ips > 0 and va_ips > 0
+    assert 0 <= tr_las <= tr_uas <= 1 and 0 <= va_las <= va_uas <= 1
+
+
 def test_bench_two_ranks_rehearsal():
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

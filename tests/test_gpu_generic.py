@@ -84,6 +84,24 @@ def test_generic_dropout_fp32_parity(ek, sk):
     assert np.abs(nodrop - ref).max() > 0.05
 
 
+@pytest.mark.parametrize("b,v,h,C", [(2, 40, 65, 2), (2, 36, 102, 3), (2, 20, 3, 2), (1, 12, 1, 1)])
+def test_generic_edge_dropout_hidden_not_multiple_of_4(b, v, h, C):
+    """The general path's masked fp32 W copies (k_pack_multi copy mode 2) at
+    hidden % 4 != 0 and hidden < 4: the last row quad of every W_c is partial,
+    and every row must still be written exactly once with its Philox mask."""
+    T = 2
+    A, h0, w = _case(b, v, h, C, seed=h * 3 + C)
+    dhT = np.random.default_rng(h).standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=0.7, state_keep=1.0, seed=98765 + h)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run_dropout(A, h0, w, T, "fp32", dr, dhT)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
 @pytest.mark.parametrize("v,h", [(120, 400), (190, 128)])
 def test_generic_empty_channel_skipping(v, h):
     """Real-data channel count (C = 92) on the general path: h_T and dL/dh0

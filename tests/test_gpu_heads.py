@@ -57,7 +57,10 @@ def test_embed_forward_backward_parity(keep):
     assert _nmax(dts[0].cpu().numpy(), rd[0] + rd[3]) <= 1e-5
     assert _nmax(dts[1].cpu().numpy(), rd[1]) <= 1e-5
     assert _nmax(dts[2].cpu().numpy(), rd[2]) <= 1e-5
-    np.testing.assert_allclose(sq.cpu().numpy(), rsq, rtol=1e-5)
+    # one squared lookup norm per TABLE, in its first segment's slot: loc's two
+    # lookups (columns 0 and 3) share one gradient, as the reference's two
+    # IndexedSlices of one variable are concatenated into one
+    np.testing.assert_allclose(sq.cpu().numpy(), [rsq[0] + rsq[3], rsq[1], rsq[2], 0.0], rtol=1e-5)
 
 
 @pytest.mark.parametrize("b,v,h,os_,keep", [(4, 20, 64, (150, 12), 1.0), (3, 37, 128, (150, 46), 0.85),
@@ -294,3 +297,28 @@ def test_run_epoch_end_to_end_reference_defaults():
     v = m.run_epoch("valid", valid, False)
     assert np.isfinite(v[0]) and 0 <= v[5] <= v[6] <= 1 and 0 <= v[16] <= 1
     assert sum(x.shape[0] for x in v[8]) == 20      # all_computed_values cover the split
+
+
+def test_run_epoch_train_with_dev_restrict_100():
+    """run_epoch on the reference's OWN sentences in its --train_with_dev mode
+    (chem_tensorflow.py:36-45: train = std dev, valid = std test) with
+    --restrict_data 100 (:248-255; the README's sample run) and the
+    reference's default params: the training loss falls over three epochs and
+    the scores are fractions."""
+    _torch()
+    from ggnn_amd.batching import TRAIN_WITH_DEV, wsj_model_sizes
+    from ggnn_amd.model import DenseGGNNChemModel
+    np.random.seed(0)
+    m = DenseGGNNChemModel(params={"compact_adjacency": True}, seed=0, **wsj_model_sizes())
+    assert m.num_channels == 92 and m.output_size_edges == 12 and m.bucket_max_nodes == 120
+    train = m.load_data(TRAIN_WITH_DEV["train_file"], True, restrict=100)
+    valid = m.load_data(TRAIN_WITH_DEV["valid_file"], False, restrict=100)
+    losses = []
+    for epoch in range(3):
+        r = m.run_epoch("epoch %d" % epoch, train, True)
+        assert np.isfinite(r[0]) and 0 <= r[5] <= r[6] <= 1
+        losses.append(r[0])
+    assert losses[-1] < losses[0]
+    va = m.run_epoch("valid", valid, False)
+    assert np.isfinite(va[0]) and 0 <= va[5] <= va[6] <= 1 and 0 <= va[16] <= 1
+    assert sum(x.shape[0] for x in va[8]) == 100
