@@ -99,10 +99,11 @@ def test_generic_edge_dropout_hidden_not_multiple_of_4(b, v, h, C):
     got = _run_dropout(A, h0, w, T, "fp32", dr, dhT)
     assert np.abs(got["hT"] - ref).max() <= FP32_TOL
     for k in GRADS:
-        # (hidden 1, C 1: dW is ONE number, a sum over 24 rows x T of single-f16
-        # operand products (the weight-gradient policy) with mixed
-        # signs; its relative error is that sum's cancellation, not the mask's)
-        tol = 5e-3 if (h == 1 and k == "edge_weights") else FP32_TOL
+        # (hidden 1: every weight gradient is one to four numbers, each a sum over
+        # 24 rows x T of single-f16 operand products (the weight-gradient
+        # policy) with mixed signs; their relative error is that
+        # sum's cancellation, not the mask's)
+        tol = 5e-3 if (h == 1 and k in ("edge_weights", "gates_kernel", "candidate_kernel")) else FP32_TOL
         assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= tol, k
 
 
