@@ -99,6 +99,45 @@ def test_forward_fp32_parity(b, v, h, C, T):
     assert np.abs(got - ref).max() <= FP32_TOL
 
 
+def test_config2_full_batch_forward_fp32_parity():
+    """configs[1] exactly as BASELINE.json names it: b = 32 synthetic dense
+    graphs, v = 64, hidden 128, e = 2 (C = 4), T = 3, forward only (SURVEY §8d
+    generator, seed 0), against the float64 reference at the fp32 bar."""
+    b, v, h, C, T = 32, 64, 128, 4, 3
+    A, h0 = O.synthetic_batch(b, v, h, C, seed=0)
+    w = O.synthetic_weights(h, C, seed=0)
+    ref, _ = O.forward(A.astype(np.float64), h0.astype(np.float64), _f64(w), T, keep_cache=False)
+    got = _run(A, h0, w, T, "fp32")["hT"]
+    assert np.abs(got - ref).max() <= FP32_TOL
+    assert _nrms(got, ref) <= 1e-5
+
+
+def test_fp16_within_1e_2_rms_on_config3_t5():
+    """north_star's 16-bit bar on configs[2]'s OWN data (config-3 shape: v = 128,
+    hidden 256, C = 8, T = 5, the SURVEY §8d dense synthetic adjacency): the
+    GGNN_FP16 mode (single f16 MFMA operands, fp32 accumulation) is within
+    1e-2 normalised RMS of the float64 reference, forward and every gradient.
+    (No policy with a bf16 operand can be, and no single-limb policy meets 1e-2
+    in max |err| there: tests/test_precision_policies.py.)"""
+    b, v, h, C, T = 8, 128, 256, 8, 5
+    A, h0 = O.synthetic_batch(b, v, h, C, seed=1)
+    w = O.synthetic_weights(h, C, seed=1)
+    dhT = np.random.default_rng(7).standard_normal((b, v, h)).astype(np.float32)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run(A, h0, w, T, "fp16", dhT=dhT)
+    errs = {"hT_nrms": _nrms(got["hT"], ref), "hT_max": float(np.abs(got["hT"] - ref).max())}
+    emu = O.forward_operand_policy(A, h0, w, T, "f16", "f16")
+    errs["emulation_hT_nrms"] = _nrms(emu, ref)
+    for k in GRADS:
+        errs[k] = _nrms(got[k].reshape(gref[k].shape), gref[k])
+    print("fp16 at config 3, T = 5:", errs)
+    assert errs["hT_nrms"] <= FP16_RMS_TOL
+    for k in GRADS:
+        assert errs[k] <= FP16_RMS_TOL, (k, errs[k])
+
+
 @pytest.mark.parametrize("b,v,h,C,T", [
     (4, 64, 256, 4, 3),     # v -> 64, N % 128 == 0: the 128-row k_gru_fwd2 outside the fused forward
     (1, 128, 256, 2, 17),   # T > FUSED_MAXT: per-timestep k_prop_fwd + k_gru_fwd2 fallback at config-3 sizes

@@ -1,0 +1,57 @@
+"""north_star's 16-bit bar ("within ... 1e-2 bf16") on configs[2]'s own data,
+decided on the oracle: the SURVEY §8d synthetic batch (b = 2 graphs of
+config 3: v = 128, hidden 256, C = 8, T = 5, Bernoulli(0.1) adjacency, in-degree
+~80, X rms ~2, a saturated GRU), forward with each MFMA precision policy's
+operand roundings (oracle.forward_operand_policy) against the float64 reference.
+
+The verdict (round 2, Missing 1) asked whether ANY 16-bit policy holds 1e-2
+there.  What the emulation shows (numbers of the full table:
+profiles/r03_precision_policies.json, tools/precision_policies.py):
+  * nothing with a bf16 operand on either side does, in normalised RMS or
+    max |err|: bf16 weights alone move h_T by > 2e-2 nrms, bf16 activations
+    alone by > 1e-2; the engine's bf16 mode is therefore held to its
+    rounding emulation and to 1e-2 on dependency trees (test_gpu_parity.py);
+  * single f16 operands on both sides (GGNN_FP16) hold 1e-2 in normalised
+    RMS but not in max |err| (a few saturated gates flip);
+  * only hi/lo limbs on BOTH sides hold 1e-2 in max |err|: f16 pairs are the
+    fp32-parity mode (<= 1e-3)."""
+import numpy as np
+import pytest
+
+import ggnn_oracle as O
+
+B, V, H, C, T = 2, 128, 256, 8, 5
+
+
+@pytest.fixture(scope="module")
+def case():
+    A, h0 = O.synthetic_batch(B, V, H, C, seed=1)
+    w = O.synthetic_weights(H, C, seed=1)
+    ref = O.forward_operand_policy(A, h0, w, T, "exact", "exact")
+    return A, h0, w, ref
+
+
+def _err(case, act, wt):
+    A, h0, w, ref = case
+    d = O.forward_operand_policy(A, h0, w, T, act, wt) - ref
+    return float(np.sqrt(np.mean(d * d) / np.mean(ref * ref))), float(np.abs(d).max())
+
+
+def test_no_bf16_operand_policy_meets_1e_2(case):
+    nrms_w, _ = _err(case, "exact", "bf16")      # bf16 weights, exact activations
+    nrms_a, _ = _err(case, "bf16", "exact")      # bf16 activations, exact weights
+    nrms_b, max_b = _err(case, "bf16", "bf16")   # the engine's bf16 mode
+    assert nrms_w > 2e-2 and nrms_a > 1e-2 and nrms_b > 2e-2 and max_b > 1e-1, (nrms_w, nrms_a, nrms_b, max_b)
+    # a bf16 hi/lo pair on the weights does not rescue bf16 activations
+    nrms_x, _ = _err(case, "bf16", "bf16x2")
+    assert nrms_x > 1e-2, nrms_x
+
+
+def test_f16_operands_meet_1e_2_in_rms_not_in_max(case):
+    nrms, mx = _err(case, "f16", "f16")          # GGNN_FP16
+    assert nrms <= 1e-2 < mx, (nrms, mx)
+
+
+def test_split_limbs_on_both_sides_meet_the_max_bar(case):
+    nrms, mx = _err(case, "f16x2", "f16x2")      # GGNN_FP32_PARITY
+    assert mx <= 1e-3 and nrms <= 1e-4, (nrms, mx)
