@@ -18,6 +18,7 @@ GGNN_FP16 = 4
 GGNN_DENSE_CHANNELS = 8
 GGNN_GENERIC = 16
 GGNN_UNFUSED_FWD = 32
+GGNN_SPARSE_PAIRS = 64
 PRECISIONS = ("bf16", "fp16", "fp32")
 
 # Every symbol include/ggnn.h declares (checked by tests/test_lib.py).
@@ -126,7 +127,7 @@ def check(rc: int, what: str) -> None:
 def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "fp32",
          edge_keep: float = 1.0, state_keep: float = 1.0, seed: int = 0,
          skip_empty_channels: bool = True, force_generic: bool = False,
-         unfused_forward: bool = False) -> GGNNDims:
+         unfused_forward: bool = False, sparse_pairs: bool = False) -> GGNNDims:
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s" % (PRECISIONS,))
     flags = (GGNN_USE_EDGE_BIAS if use_edge_bias else 0) | {"bf16": 0, "fp16": GGNN_FP16, "fp32": GGNN_FP32_PARITY}[precision]
@@ -136,6 +137,8 @@ def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, pre
         flags |= GGNN_GENERIC
     if unfused_forward:
         flags |= GGNN_UNFUSED_FWD
+    if sparse_pairs:
+        flags |= GGNN_SPARSE_PAIRS
     return GGNNDims(int(b), int(v), int(h), int(C), int(T), flags, float(edge_keep), float(state_keep),
                     int(seed) & 0xFFFFFFFFFFFFFFFF)
 

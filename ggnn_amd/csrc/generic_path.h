@@ -20,6 +20,9 @@ struct GenAdjL {
   size_t Ag, AgT, occ, chl, cgl, cgc, total;
   int vp;
   int nch, gch;  // cgc: every channel's graph list cut into nch chunks of <= gch graphs
+  // pair mode (GGNN_SPARSE_PAIRS, k_pairs.h)
+  size_t degc, pidx, pcnt, poff, prow, pdeg, ptile, pmask, wtl, wmap, wmask;
+  int cap_tiles, zw;  // product tiles of the pair-row capacity; dW split-K chunks
 };
 GenAdjL gen_adj_layout(const Cfg& c) {
   GenAdjL L;
@@ -39,12 +42,29 @@ GenAdjL gen_adj_layout(const Cfg& c) {
   L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);
   L.cgl = o; o += al((size_t)c.C * (c.b + 1) * 4);
   L.cgc = o; o += al((size_t)c.C * L.nch * (L.gch + 1) * 4);
+  L.cap_tiles = (int)(c.pcap / PAIR_TILE);
+  L.zw = c.sparse ? L.cap_tiles / PAIR_CHUNK + c.C : 0;
+  if (c.sparse) {
+    const size_t N = (size_t)c.b * c.vin;
+    L.degc = o;  o += al((size_t)c.C * N * 2);
+    L.pidx = o;  o += al((size_t)c.C * N * 4);
+    L.pcnt = o;  o += al((size_t)c.C * 4);
+    L.poff = o;  o += al((size_t)(c.C + 1) * 4);
+    L.prow = o;  o += al((size_t)c.pcap * 4);
+    L.pdeg = o;  o += al((size_t)c.pcap * 4);
+    L.ptile = o; o += al((size_t)L.cap_tiles * 2 * 4);
+    L.pmask = o; o += al((size_t)L.cap_tiles);
+    L.wtl = o;   o += al((size_t)L.zw * (1 + PAIR_CHUNK) * 4);
+    L.wmap = o;  o += al((size_t)L.zw * 4);
+    L.wmask = o; o += al((size_t)L.zw);
+  }
   L.total = o;
   return L;
 }
 
 struct GenWsL {
   size_t hs, X, G, RH, CC, M, Dl, DXH, DZC, DZG, DRH, GW, gmax, total;
+  size_t PY, PZ, PDX;  // pair mode: Y = A h, Z = Y W (dY in the backward), dX gathered, [pcap][H] each
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
   size_t hsl(int t) const { return hs + (size_t)t * nh * 4; }
   size_t x(int t) const { return X + (size_t)(t % ns) * nh * 4; }
@@ -66,14 +86,20 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
   L.G = o;   o += 2 * a4 * L.ns;
   L.RH = o;  o += a4 * L.ns;
   L.CC = o;  o += a4 * L.ns;
-  L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
+  if (c.sparse) {
+    L.PY = o;  o += al((size_t)c.pcap * H * 4);
+    L.PZ = o;  o += al((size_t)c.pcap * H * 4);
+    if (tr) { L.PDX = o; o += al((size_t)c.pcap * H * 4); }
+  } else {
+    L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
+  }
   if (tr) {
     L.Dl = o;  o += a4;
     L.DXH = o; o += 2 * a4;
     L.DZC = o; o += a4;
     L.DZG = o; o += 2 * a4;
     L.DRH = o; o += a4;
-    if (c.ed) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
+    if (c.ed && !c.sparse) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
     L.gmax = o; o += al(4);
   }
   L.total = o;
@@ -223,7 +249,46 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
     hipLaunchKernelGGL(k_gen_adj_edges, dim3((unsigned)std::min(c.b, 4096)), dim3(256), 0, s, edges, goff, c.b, c.vin,
                        L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<u16>(adj, L.AgT),
                        P<unsigned char>(adj, L.occ));
+  if (c.sparse) {
+    // pair rows grouped by channel (k_pairs.h S1-S4)
+    const long N = (long)c.b * c.vin;
+    hipLaunchKernelGGL(k_pair_degree, dim3((unsigned)(c.b * c.C)), dim3(256), 0, s, P<const u16>(adj, L.Ag),
+                       P<const unsigned char>(adj, L.occ), c.b, c.C, c.vin, L.vp, P<u16>(adj, L.degc));
+    hipLaunchKernelGGL(k_pair_scan, dim3((unsigned)c.C), dim3(1024), 0, s, P<const u16>(adj, L.degc), N,
+                       P<int>(adj, L.pidx), P<int>(adj, L.pcnt));
+    hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
+                       P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
+                       P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask));
+    HIPCHK(hipMemsetAsync(P<int>(adj, L.prow), 0xFF, (size_t)c.pcap * 4, s));
+    HIPCHK(hipMemsetAsync(P<float>(adj, L.pdeg), 0, (size_t)c.pcap * 4, s));
+    hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
+                       P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
+                       P<int>(adj, L.prow), P<float>(adj, L.pdeg));
+  }
   return GGNN_OK;
+}
+
+// pair mode, Y = A h over the pair rows (forward F1; recomputed in the backward)
+void gen_pairs_y(const Cfg& c, const GenAdjL& AL, const void* adj, const float* h, float* Y, hipStream_t s) {
+  const unsigned grid = (unsigned)std::min<long>((c.pcap + 3) / 4, 16384);
+  hipLaunchKernelGGL(k_pair_gather_y, dim3(grid), dim3(256), 0, s, P<const u16>(adj, AL.Ag), P<const int>(adj, AL.prow),
+                     P<const int>(adj, AL.ptile), P<const unsigned char>(adj, AL.pmask), h, Y, c.C, c.vin, AL.vp, c.H,
+                     (int)c.pcap);
+}
+// the per-tile product Z = A_op W_c (forward: A_op = Y, B = W; backward: A_op =
+// dXg, B = W^T): z = 32-row tile, its channel from the one-entry term list
+template <int PREC>
+int gen_pairs_product(const Cfg& c, const GenAdjL& AL, const void* adj, const float* Aop, const float* W, bool wt,
+                      float* D, int kind, hipStream_t s) {
+  const long H = c.H;
+  GemmArgs z = gg_args();
+  z.A = Aop; z.sAp = PAIR_TILE * H; z.sAm = H; z.sAk = 1;
+  z.B = W; z.sBq = H * H;
+  if (wt) { z.sBk = 1; z.sBn = H; } else { z.sBk = H; z.sBn = 1; }
+  z.D = D; z.sDz = PAIR_TILE * H; z.sDm = H; z.sDn = 1;
+  z.tl = P<const int>(adj, AL.ptile); z.ts = 2; z.zmask = P<const unsigned char>(adj, AL.pmask);
+  z.Z = AL.cap_tiles; z.M = PAIR_TILE; z.N = (int)H; z.K = (int)H;
+  return gg_launch<PREC>(z, false, true, wt, kind, s);
 }
 // channel lists of the staged batch (per graph, per channel); rebuilt by every
 // forward so that GGNN_DENSE_CHANNELS can be chosen per call
@@ -253,6 +318,25 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
   for (int t = 0; t < c.T; ++t) {
     const size_t hin = tr ? L.hsl(t) : L.hsl(t & 1);
     float* hout = (t + 1 == c.T) ? hT : P<float>(ws, tr ? L.hsl(t + 1) : L.hsl((t + 1) & 1));
+    if (c.sparse) {
+      // pair mode (k_pairs.h): Y = A h, Z = Y W_c per 32-row tile, X = the
+      // row's sum of Z + deg beta
+      float* PY = P<float>(ws, L.PY);
+      float* PZ = P<float>(ws, L.PZ);
+      {
+        Prof p(K_PROP_FWD, s);
+        gen_pairs_y(c, AL, adj, P<const float>(ws, hin), PY, s);
+      }
+      if (int e = gen_pairs_product<PREC>(c, AL, adj, PY, P<float>(pack, PL.gw(c.ed ? t : 0)), false, PZ, K_PROP_FWD,
+                                          s))
+        return e;
+      {
+        Prof p(K_PROP_FWD, s);
+        hipLaunchKernelGGL(k_pair_reduce_x, dim3(grid1d(N * (H / 4))), dim3(256), 0, s, P<const int>(adj, AL.pidx),
+                           P<const float>(adj, AL.pdeg), P<const int>(adj, AL.chl), PZ, beta, P<float>(ws, L.x(t)), N,
+                           c.vin, c.C, c.H);
+      }
+    } else {
     // M[g,c] = h_t[g] W_c + beta_c over the non-empty (g, c) tiles
     GemmArgs m = gg_args();
     m.A = P<float>(ws, hin); m.sAp = v * H; m.sAm = H; m.sAk = 1;
@@ -270,6 +354,7 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     x.tl = P<int>(adj, AL.chl); x.ts = C + 1;
     x.Z = c.b; x.M = (int)v; x.N = (int)H; x.K = (int)v;
     if (int e = gg_launch<PREC>(x, true, true, false, K_PROP_FWD, s)) return e;
+    }
     // gates = sigmoid([X, h] Wg + bg)
     GemmArgs gt = gg_args();
     gt.A = P<float>(ws, L.x(t)); gt.sAq = ((long)hin - (long)L.x(t)) / 4; gt.sAm = H; gt.sAk = 1;
@@ -390,6 +475,45 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     if (int e = wg(P<float>(ws, L.rh(t)), DZC, H, (int)H, dWc + H * H, H)) return e;
     if (int e = wg(P<float>(ws, L.x(t)), DZG, 2 * H, (int)(2 * H), dWg, 2 * H)) return e;
     if (int e = wg(ht, DZG, 2 * H, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
+    if (c.sparse) {
+      // pair mode (k_pairs.h): Y_t recomputed from the saved h_t, dXg = dX
+      // of the pair rows, dbeta, dY = dXg W_c^T, dh += A^T dY, dW_c += Y^T dXg
+      float* PY = P<float>(ws, L.PY);
+      float* PZ = P<float>(ws, L.PZ);
+      float* PDX = P<float>(ws, L.PDX);
+      {
+        Prof p(K_PROP_BWD, s);
+        gen_pairs_y(c, AL, adj, ht, PY, s);
+        hipLaunchKernelGGL(k_pair_gather_dx, dim3(grid1d(c.pcap * (H / 4))), dim3(256), 0, s,
+                           P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask), DXH, PDX, (int)c.pcap,
+                           c.H);
+        if (use_bias)
+          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C, 8), dim3(256), 0, s,
+                             P<const int>(adj, AL.poff), P<const int>(adj, AL.pcnt), P<const float>(adj, AL.pdeg), PDX,
+                             dbeta, c.H);
+      }
+      if (int e = gen_pairs_product<PREC>(c, AL, adj, PDX, P<float>(pack, PL.gw(c.ed ? t : 0)), true, PZ, K_PROP_BWD,
+                                          s))
+        return e;
+      {
+        Prof p(K_PROP_BWD, s);
+        hipLaunchKernelGGL(k_pair_scatter_dh, dim3((unsigned)std::min<long>((N + 3) / 4, 16384)), dim3(256), 0, s,
+                           P<const u16>(adj, AL.AgT), P<const int>(adj, AL.chl), P<const int>(adj, AL.pidx), PZ, DXH,
+                           c.b, c.vin, AL.vp, c.C, c.H);
+      }
+      // dW_c += Y_c^T dXg_c: z = a chunk of <= PAIR_CHUNK tiles of one channel
+      // (zmap), one term per tile, fp32 atomics; under edge dropout the mask
+      // of timestep t is applied in the epilogue (no per-timestep slab)
+      GemmArgs a = gg_args();
+      a.A = PY; a.sAm = 1; a.sAk = H; a.sAq = PAIR_TILE * H;
+      a.B = PDX; a.sBk = H; a.sBn = 1; a.sBq = PAIR_TILE * H;
+      a.D = dW; a.sDp = H * H; a.sDm = H; a.sDn = 1; a.mode = GG_ATOMIC;
+      a.tl = P<const int>(adj, AL.wtl); a.ts = 1 + PAIR_CHUNK;
+      a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
+      a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
+      if (c.ed) { a.dr = c.edrop; a.drop_t = t; }
+      if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
+    } else {
     // dM[g,c] = A[g,c]^T dX[g] over the non-empty tiles
     {
       GemmArgs a = gg_args();
@@ -429,6 +553,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       if (c.ed)
         hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * ((H + 3) / 4) * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
                            c.C, c.H, t, c.edrop);
+    }
     }
     // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
     {

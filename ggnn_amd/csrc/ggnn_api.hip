@@ -23,6 +23,7 @@
 #include "k_gemm.h"
 #include "k_gemm_ring.h"
 #include "k_generic.h"
+#include "k_pairs.h"
 
 // ---------------------------------------------------------------------------
 // error handling (thread-local last error; no exception crosses the ABI)
@@ -83,6 +84,8 @@ struct Cfg {
   Drop edrop, sdrop;  // edge-weight / state dropout (thr == 0: off)
   bool ed, sd;
   bool generic;       // the general path (generic_path.h)
+  bool sparse;        // GGNN_SPARSE_PAIRS (k_pairs.h)
+  long pcap;          // pair-row capacity (sparse): 4 * b * v + PAIR_TILE * C, a multiple of PAIR_TILE
 };
 
 Drop make_drop(float keep, uint64_t seed) {
@@ -107,11 +110,14 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   if (d->b < 1 || d->v < 1 || d->C < 1 || d->T < 1) return fail(GGNN_EINVAL, "dims: b, v, C, T must be >= 1");
   if (d->h < 1 || d->h > 4096) return fail(GGNN_EUNSUP, "hidden size must lie in 1..4096 (got " + std::to_string(d->h) + ")");
   if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS | GGNN_GENERIC |
-                   GGNN_UNFUSED_FWD))
+                   GGNN_UNFUSED_FWD | GGNN_SPARSE_PAIRS))
     return fail(GGNN_EINVAL, "unknown flag bits");
   // the specialised kernels: hidden 128 / 256, v <= 128; everything else runs
-  // the general path (generic_path.h)
-  c->generic = (d->flags & GGNN_GENERIC) || !(d->h == 128 || d->h == 256) || d->v > 128;
+  // the general path (generic_path.h); pair mode is part of it
+  c->sparse = (d->flags & GGNN_SPARSE_PAIRS) != 0;
+  if (c->sparse && d->h % 4) return fail(GGNN_EUNSUP, "GGNN_SPARSE_PAIRS needs hidden % 4 == 0");
+  c->generic = c->sparse || (d->flags & GGNN_GENERIC) || !(d->h == 128 || d->h == 256) || d->v > 128;
+  c->pcap = c->sparse ? 4L * d->b * d->v + (long)PAIR_TILE * d->C : 0;
   const int V = c->generic ? d->v : pad_v(d->v);
   if (d->C > CHL_MAXC) return fail(GGNN_EUNSUP, "C must be <= " + std::to_string(CHL_MAXC));
   if ((d->flags & GGNN_FP32_PARITY) && (d->flags & GGNN_FP16))
@@ -884,6 +890,8 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
   if (num_edge_types < 1 || 2 * num_edge_types != c.C)
     return fail(GGNN_EINVAL, "set_adjacency_edges: C must equal 2 * num_edge_types");
   if (num_edges < 0) return fail(GGNN_EINVAL, "set_adjacency_edges: num_edges < 0");
+  if (c.sparse && num_edges > (int64_t)c.b * c.vin)
+    return fail(GGNN_EUNSUP, "set_adjacency_edges: GGNN_SPARSE_PAIRS needs num_edges <= b * v");
   hipStream_t s = (hipStream_t)stream;
   if (c.generic) {
     if (int e2 = gen_set_adjacency_edges(c, adj, edges, graph_offsets, num_edges, num_edge_types, s)) return e2;
@@ -920,6 +928,7 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
   int e = make_cfg(d, &c);
   if (e) return e;
   if (!adj || !A) return fail(GGNN_EINVAL, "set_adjacency: NULL pointer");
+  if (c.sparse) return fail(GGNN_EINVAL, "set_adjacency: GGNN_SPARSE_PAIRS batches are staged by set_adjacency_edges");
   hipStream_t s = (hipStream_t)stream;
   if (c.generic) {
     if (int e2 = gen_set_adjacency(c, adj, A, s)) return e2;

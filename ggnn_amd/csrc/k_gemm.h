@@ -66,6 +66,15 @@ struct GemmArgs {
   // wave pair
   float* csum;
   long scp, scq;
+  // if set: zp = zmap[z], zq = 0 (z -> an arbitrary operand group, e.g. the
+  // pair-mode dW chunks of channel zmap[z], k_pairs.h)
+  const int* zmap;
+  // if dr.thr: every stored value (m, n) of z is multiplied by the edge-dropout
+  // mask of (channel zp, row m, column n, timestep drop_t) / keep -- the
+  // masked weight gradient dW_c += mask_t * (Y^T dX) accumulated straight into
+  // dW (Philox counter (m>>2, n, zp, t), word m&3: one block per row quad)
+  Drop dr;
+  int drop_t;
 };
 
 namespace gg {
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 
   for (int z = blockIdx.z; z < a.Z; z += gridDim.z) {
     if (a.zmask && !a.zmask[z]) continue;
-    const int zp = z / a.zdiv, zq = z % a.zdiv;
+    const int zp = a.zmap ? a.zmap[z] : z / a.zdiv, zq = a.zmap ? 0 : z % a.zdiv;
     const int nt = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
     const int nst = nt * kc;
     auto term = [&](int e, int& p, int& q) {
@@ -297,15 +306,18 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
       if (n < a.N) {
         const float bn = bias ? bias[n] : 0.f;
         const bool hi_n = a.Nsplit && n >= a.Nsplit;
+        uint4 dq = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int i = 0; i < WM; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
+            if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
             if (m >= a.M) continue;
             float x = a.alpha * acc[i][j][r] + bn;
             if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
             else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+            if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);
             const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
             if (a.E) x *= a.E[doff];
             cs += x;

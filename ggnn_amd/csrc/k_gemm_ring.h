@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   // and meets every barrier, but reads no fragments and issues no MFMAs
   const bool live = __builtin_amdgcn_readfirstlane((int)(n0 + wn * AN * 32 < a.N && m0 + wm * AM * 32 < a.M));
   const int kc = (a.K + BK - 1) / BK;
-  const int zp = z / a.zdiv, zq = z % a.zdiv;
+  const int zp = a.zmap ? a.zmap[z] : z / a.zdiv, zq = a.zmap ? 0 : z % a.zdiv;
   const int nterms = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
   const int nit = nterms * kc;
   // z's first 128 terms in two VGPRs (lane l: terms l and 64 + l), fetched
@@ -290,15 +290,18 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
     if (n < a.N) {
       const float bn = bias ? bias[n] : 0.f;
       const bool hi_n = a.Nsplit && n >= a.Nsplit;
+      uint4 dq = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
       for (int i = 0; i < AM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
+          if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
           if (m >= a.M) continue;
           float x = a.alpha * acc[i][j][r] + bn;
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+          if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);
           const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
           if (a.E) x *= a.E[doff];
           cs += x;

@@ -1,0 +1,308 @@
+// k_pairs.h -- the general path's sparse message passing ("pair mode",
+// GGNN_SPARSE_PAIRS) for adjacency with few edges per node, e.g. the
+// reference's dependency trees (C = 92 channels, ~0.1 % density, ~4
+// (node, channel) pairs with an incoming edge per node).
+//
+// The reference contracts X[g,i] = sum_c sum_j A[g,c,i,j] (h[g,j] W_c + beta_c)
+// (chem_tensorflow_dense.py:391-437).  The dense tile path computes
+// M[g,c] = h[g] W_c for EVERY row of every non-empty (graph, channel) tile
+// (~26 tiles x v rows per sentence graph), then the adjacency product.  Pair
+// mode re-associates the same sum as
+//   X[g,i] = sum over pairs p = (g,i,c) with deg_p = sum_j A[g,c,i,j] > 0 of
+//            Y_p W_c + deg_p beta_c,          Y_p = sum_j A[g,c,i,j] h[g,j]
+// so the message transform runs over the ~4 pair rows per node instead of
+// ~26 tile rows, and W_c streams once per 32 pair rows of channel c.
+//
+// Pair rows are grouped by channel, each channel's range padded to a multiple
+// of PAIR_TILE rows, so a 32-row product tile has ONE channel: the products
+// are ordinary k_gemm_ring launches whose z = tile carries its channel as a
+// one-entry term list (ptile).  Built once per staged batch on the device
+// (k_pair_degree / _scan / _layout / _fill); every sum is in a fixed order, so
+// the results are deterministic.  Backward (same
+// decomposition): dXg_p = dX[row_p]; dY = dXg W_c^T; dh[g,j] += sum over pairs
+// with A[g,c,i,j] = 1 of dY_p; dW_c += Y_c^T dXg_c (split-K over chunks of
+// PAIR_CHUNK tiles, the edge-dropout mask applied in the product's epilogue);
+// dbeta_c += sum_p deg_p dXg_p.
+#pragma once
+#include "ggnn_common.h"
+
+#define PAIR_TILE 32   // rows per product tile (the ring kernel's 32-row variant)
+#define PAIR_CHUNK 16  // tiles per split-K term list of the dW product (512 rows)
+
+// S1: in-degree per (channel, node row) from the staged 16-bit rows (0/1
+// limbs: nonzero bits <=> 1); one block per (graph, channel) tile, a wave per row
+__global__ void __launch_bounds__(256) k_pair_degree(const u16* __restrict__ Ag, const unsigned char* __restrict__ occ,
+                                                     int b, int C, int v, int vp, u16* __restrict__ degc) {
+  const int tile = blockIdx.x, g = tile / C, c = tile - g * C;
+  const long N = (long)b * v;
+  u16* out = degc + (long)c * N + (long)g * v;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (!occ[tile]) {
+    for (int i = tid; i < v; i += 256) out[i] = 0;
+    return;
+  }
+  for (int i = w; i < v; i += 4) {
+    const u16* row = Ag + ((long)tile * v + i) * vp;
+    int cnt = 0;
+    for (int j = lane; j < vp; j += 64) cnt += row[j] != 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane == 0) out[i] = (u16)cnt;
+  }
+}
+
+// S2: per channel (one block), the position of every node row with an
+// incoming edge among the channel's pair rows (ascending node order), -1
+// elsewhere; pcnt[c] = the channel's pair count
+__global__ void __launch_bounds__(1024) k_pair_scan(const u16* __restrict__ degc, long N, int* __restrict__ pidx,
+                                                    int* __restrict__ pcnt) {
+  const int c = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const u16* d = degc + (long)c * N;
+  int* o = pidx + (long)c * N;
+  __shared__ int wsum[16];
+  int base = 0;
+  for (long r0 = 0; r0 < N; r0 += 1024) {
+    const long r = r0 + tid;
+    const int f = r < N && d[r] != 0;
+    const unsigned long long m = __ballot(f);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      woff += u < w ? wsum[u] : 0;
+      tot += wsum[u];
+    }
+    if (r < N) o[r] = f ? base + woff + pre : -1;
+    base += tot;
+    __syncthreads();  // wsum is rewritten by the next chunk
+  }
+  if (tid == 0) pcnt[c] = base;
+}
+
+// S3: channel offsets (padded to PAIR_TILE), the per-tile term lists of the
+// products (ptile[2z] = 1 live / 0 dead, ptile[2z+1] = channel; pmask), and the
+// dW product's split-K chunks (wtl[z*(1+PAIR_CHUNK)] = tile count, then the
+// tile indices; wmap[z] = channel; wmask).  One block.
+__global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pcnt, int C, int cap_tiles, int zw_cap,
+                                                      int* __restrict__ poff, int* __restrict__ ptile,
+                                                      unsigned char* __restrict__ pmask, int* __restrict__ wtl,
+                                                      int* __restrict__ wmap, unsigned char* __restrict__ wmask) {
+  __shared__ int soff[CHL_MAXC + 1], cst[CHL_MAXC + 1];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int off = 0, ch = 0;
+    for (int c = 0; c < C; ++c) {
+      soff[c] = off;
+      cst[c] = ch;
+      const int t = (pcnt[c] + PAIR_TILE - 1) / PAIR_TILE;
+      off += t * PAIR_TILE;
+      ch += (t + PAIR_CHUNK - 1) / PAIR_CHUNK;
+    }
+    soff[C] = off;
+    cst[C] = ch;
+  }
+  __syncthreads();
+  for (int c = tid; c <= C; c += blockDim.x) poff[c] = soff[c];
+  const int live_tiles = soff[C] / PAIR_TILE;
+  // the channel of a tile / chunk: the last c with start <= x (binary search)
+  auto find = [&](const int* st, int x) {
+    int lo = 0, hi = C - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (st[mid] <= x) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  for (int z = tid; z < cap_tiles; z += blockDim.x) {
+    const bool live = z < live_tiles;
+    ptile[2 * z] = live ? 1 : 0;
+    ptile[2 * z + 1] = live ? find(soff, z * PAIR_TILE) : 0;
+    pmask[z] = live ? 1 : 0;
+  }
+  for (int z = tid; z < zw_cap; z += blockDim.x) {
+    int* q = wtl + (long)z * (1 + PAIR_CHUNK);
+    if (z < cst[C]) {
+      const int c = find(cst, z), j = z - cst[c];
+      const int t0 = soff[c] / PAIR_TILE, nt = (soff[c + 1] - soff[c]) / PAIR_TILE;
+      const int cnt = min(PAIR_CHUNK, nt - j * PAIR_CHUNK);
+      q[0] = cnt;
+      for (int e = 0; e < cnt; ++e) q[1 + e] = t0 + j * PAIR_CHUNK + e;
+      wmap[z] = c;
+      wmask[z] = 1;
+    } else {
+      q[0] = 0;
+      wmap[z] = 0;
+      wmask[z] = 0;
+    }
+  }
+}
+
+// S4: pair rows: prow[p] = node row, pdeg[p] = in-degree; pidx[c][r] becomes
+// the global pair row of (r, c) (or -1).  prow / pdeg were set to -1 / 0.
+__global__ void k_pair_fill(const u16* __restrict__ degc, int* __restrict__ pidx, const int* __restrict__ poff, long N,
+                            long total, int cap, int* __restrict__ prow, float* __restrict__ pdeg) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int pos = pidx[e];
+    if (pos < 0) continue;
+    const int c = (int)(e / N);
+    const long r = e - (long)c * N;
+    const int p = poff[c] + pos;
+    if (p < cap) {
+      prow[p] = (int)r;
+      pdeg[p] = (float)degc[e];
+    }
+    pidx[e] = p < cap ? p : -1;
+  }
+}
+
+// F1 (and its recomputation in the backward): Y[p][k] = sum_j A[g,c,i,j] h[g*v+j][k]
+// for every pair row p = (g*v+i, c) of a live tile; padding rows of a live
+// tile get zeros (the products read whole tiles).  One wave per pair row,
+// 4 columns per lane (H % 4 == 0), the row's sources found by ballots over the
+// staged adjacency row.
+__global__ void __launch_bounds__(256) k_pair_gather_y(const u16* __restrict__ Ag, const int* __restrict__ prow,
+                                                       const int* __restrict__ ptile,
+                                                       const unsigned char* __restrict__ pmask,
+                                                       const float* __restrict__ h, float* __restrict__ Y, int C,
+                                                       int v, int vp, int H, int rows) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < rows; p += nw) {
+    if (!pmask[p / PAIR_TILE]) continue;
+    const int r = prow[p];
+    float* y = Y + (long)p * H;
+    if (r < 0) {
+      for (int k = 4 * lane; k < H; k += 256) *(float4*)(y + k) = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
+    const int c = ptile[2 * (p / PAIR_TILE) + 1];
+    const int g = r / v, i = r - g * v;
+    const u16* arow = Ag + (((long)g * C + c) * v + i) * vp;
+    const float* hg = h + (long)g * v * H;
+    for (int k0 = 0; k0 < H; k0 += 256) {
+      const int k = k0 + 4 * lane;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int jb = 0; jb < v; jb += 64) {
+        const int j = jb + lane;
+        unsigned long long m = __ballot(j < v && arow[j] != 0);
+        while (m) {
+          const int jj = jb + __ffsll((long long)m) - 1;
+          m &= m - 1ull;
+          if (k < H) {
+            const float4 x = *(const float4*)(hg + (long)jj * H + k);
+            acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+          }
+        }
+      }
+      if (k < H) *(float4*)(y + k) = acc;
+    }
+  }
+}
+
+// F3: X[r][k] = sum over the channels c of r's graph (ascending) with a pair
+// (r, c) of Z[p][k] + deg_p beta[c][k]; one thread per (row, column quad)
+__global__ void k_pair_reduce_x(const int* __restrict__ pidx, const float* __restrict__ pdeg,
+                                const int* __restrict__ chl, const float* __restrict__ Z,
+                                const float* __restrict__ beta, float* __restrict__ X, long N, int v, int C, int H) {
+  const int hq = H >> 2;
+  const long total = N * hq;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / hq;
+    const int k = 4 * (int)(e - r * hq);
+    const int g = (int)(r / v);
+    const int* cl = chl + (long)g * (C + 1);
+    const int n = cl[0];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < n; ++u) {
+      const int c = cl[1 + u];
+      const int p = pidx[(long)c * N + r];
+      if (p < 0) continue;
+      const float4 z = *(const float4*)(Z + (long)p * H + k);
+      acc.x += z.x; acc.y += z.y; acc.z += z.z; acc.w += z.w;
+      if (beta) {
+        const float d = pdeg[p];
+        const float4 bb = *(const float4*)(beta + (long)c * H + k);
+        acc.x += d * bb.x; acc.y += d * bb.y; acc.z += d * bb.z; acc.w += d * bb.w;
+      }
+    }
+    *(float4*)(X + r * H + k) = acc;
+  }
+}
+
+// B1: dXg[p] = dX[prow[p]] (dX = the first half of the [N][2H] DXH rows); 0 on
+// the padding rows of live tiles
+__global__ void k_pair_gather_dx(const int* __restrict__ prow, const unsigned char* __restrict__ pmask,
+                                 const float* __restrict__ DXH, float* __restrict__ dXg, int rows, int H) {
+  const int hq = H >> 2;
+  const long total = (long)rows * hq;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(e / hq), k = 4 * (int)(e - (long)p * hq);
+    if (!pmask[p / PAIR_TILE]) continue;
+    const int r = prow[p];
+    const float4 x = r >= 0 ? *(const float4*)(DXH + (long)r * 2 * H + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dXg + (long)p * H + k) = x;
+  }
+}
+
+// dbeta[c][k] += sum over c's pair rows of deg_p dXg[p][k]: grid (column
+// blocks, C, row slices), one atomic per column per block
+__global__ void __launch_bounds__(256) k_pair_dbeta(const int* __restrict__ poff, const int* __restrict__ pcnt,
+                                                    const float* __restrict__ pdeg, const float* __restrict__ dXg,
+                                                    float* __restrict__ dbeta, int H) {
+  const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+  if (k >= H) return;
+  const int n = pcnt[c], p0 = poff[c];
+  const int per = (n + gridDim.z - 1) / gridDim.z, a = blockIdx.z * per, e = min(n, a + per);
+  if (a >= e) return;
+  float s = 0.f;
+  for (int p = p0 + a; p < p0 + e; ++p) s += pdeg[p] * dXg[(long)p * H + k];
+  atomicAdd(dbeta + (long)c * H + k, s);
+}
+
+// B3: DXH[g*v+j][H + k] += sum over the channels c of g (ascending) and the
+// receivers i of j on c (A[g,c,i,j] = 1, ascending) of dY[pair(g*v+i, c)][k];
+// one wave per source row, the receivers found by ballots over the staged
+// transpose AgT
+__global__ void __launch_bounds__(256) k_pair_scatter_dh(const u16* __restrict__ AgT, const int* __restrict__ chl,
+                                                         const int* __restrict__ pidx, const float* __restrict__ dY,
+                                                         float* __restrict__ DXH, int b, int v, int vp, int C, int H) {
+  const int lane = threadIdx.x & 63;
+  const long N = (long)b * v;
+  const int nw = gridDim.x * 4;
+  for (long r = blockIdx.x * 4 + (threadIdx.x >> 6); r < N; r += nw) {
+    const int g = (int)(r / v), j = (int)(r - (long)g * v);
+    const int* cl = chl + (long)g * (C + 1);
+    const int n = cl[0];
+    for (int k0 = 0; k0 < H; k0 += 256) {
+      const int k = k0 + 4 * lane;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < n; ++u) {
+        const int c = cl[1 + u];
+        const u16* arow = AgT + (((long)g * C + c) * v + j) * vp;
+        const int* pc = pidx + (long)c * N + (long)g * v;
+        for (int ib = 0; ib < v; ib += 64) {
+          const int i = ib + lane;
+          unsigned long long m = __ballot(i < v && arow[i] != 0);
+          while (m) {
+            const int ii = ib + __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const int p = pc[ii];
+            if (p >= 0 && k < H) {
+              const float4 x = *(const float4*)(dY + (long)p * H + k);
+              acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+            }
+          }
+        }
+      }
+      if (k < H) {
+        float4* d = (float4*)(DXH + r * 2 * H + H + k);
+        float4 o = *d;
+        o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+        *d = o;
+      }
+    }
+  }
+}

@@ -60,7 +60,7 @@ class PropagationEngine:
 
     def __init__(self, hidden: int, channels: int, use_edge_bias: bool = True, device=None,
                  precision: str = "fp32", skip_empty_channels: bool = True, force_generic: bool = False,
-                 unfused_forward: bool = False):
+                 unfused_forward: bool = False, sparse_pairs="auto"):
         """precision: "fp32" (GGNN_FP32_PARITY, the default: every non-exact MFMA
         operand of the propagation as an f16 hi/lo limb pair, fp32 accumulation,
         matches the reference's fp32 math to <= 1e-3), "fp16" or "bf16" (single
@@ -71,7 +71,15 @@ class PropagationEngine:
         specialised kernels apply (hidden 128 / 256, v <= 128); other shapes
         always take it (GGNN_GENERIC).  unfused_forward: per-timestep
         k_prop_fwd + k_gru_fwd launches instead of the one-launch fused forward
-        at hidden 256, v <= 128 (GGNN_UNFUSED_FWD; A/B and tests)."""
+        at hidden 256, v <= 128 (GGNN_UNFUSED_FWD; A/B and tests).
+        sparse_pairs: the general path's sparse message passing
+        (GGNN_SPARSE_PAIRS: the message transform over the (node, channel)
+        pairs with an incoming edge instead of every row of every non-empty
+        tile) for batches staged from edge lists: "auto" = whenever such a
+        batch runs the general path anyway (hidden not 128 / 256, v > 128 or
+        force_generic) and qualifies (hidden % 4 == 0, edges <= b*v); True =
+        for every qualifying edge-list batch (also hidden 128 / 256: pair mode
+        implies the general path); False = never."""
         self.h = int(hidden)
         self.C = int(channels)
         self.use_edge_bias = bool(use_edge_bias)
@@ -82,6 +90,10 @@ class PropagationEngine:
         self.skip_empty_channels = bool(skip_empty_channels)
         self.force_generic = bool(force_generic)
         self.unfused_forward = bool(unfused_forward)
+        if sparse_pairs not in ("auto", True, False):
+            raise ValueError("sparse_pairs must be 'auto', True or False")
+        self.sparse_pairs = sparse_pairs
+        self._sparse = False        # the staged batch runs pair mode
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._lib = _lib.load()
         self._adj = None            # staged adjacency buffer
@@ -94,12 +106,12 @@ class PropagationEngine:
     def dims(self, b: int, v: int, T: int, edge_keep: float = 1.0, state_keep: float = 1.0,
              seed: int = 0) -> _lib.GGNNDims:
         d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision, edge_keep, state_keep, seed,
-                      self.skip_empty_channels, self.force_generic, self.unfused_forward)
+                      self.skip_empty_channels, self.force_generic, self.unfused_forward, self._sparse)
         _lib.check_dims(d)
         return d
 
     def workspace(self, b: int, v: int, T: int, training: bool, edge_dropout: bool = False) -> torch.Tensor:
-        key = (b, v, T, bool(training), bool(edge_dropout))
+        key = (b, v, T, bool(training), bool(edge_dropout), self._sparse)
         ws = self._ws.get(key)
         if ws is None:
             if len(self._ws) >= 4:      # keep a handful of shapes (bucketed batches)
@@ -145,6 +157,7 @@ class PropagationEngine:
             raise ValueError("adjacency must be [b, %d, v, v], got %s" % (self.C, tuple(adjacency.shape)))
         b, _, v, _ = adjacency.shape
         _require(adjacency, (b, self.C, v, v), "adjacency")
+        self._sparse = False          # (pair mode is staged from edge lists only)
         d = self.dims(b, v, 1)
         nbytes = _lib.adjacency_bytes(d)
         if self._adj is None or self._adj.numel() < nbytes:
@@ -186,6 +199,7 @@ class PropagationEngine:
                     raise IndexError("edge node index outside 0..%d" % (v - 1))
             edges = self._up_edges(e_np, self.device)
             offs = self._up_offs(offs_np, self.device)
+        self._sparse = self._use_pairs(b, v, n)
         d = self.dims(b, v, 1)
         nbytes = _lib.adjacency_bytes(d)
         if self._adj is None or self._adj.numel() < nbytes:
@@ -194,6 +208,19 @@ class PropagationEngine:
                                                       n, E, _stream()), "ggnn_set_adjacency_edges")
         self._batch = (int(b), int(v))
         self._trained = None
+
+    def _use_pairs(self, b: int, v: int, n_edges: int) -> bool:
+        """Pair mode for this edge-list batch (see __init__'s sparse_pairs)."""
+        if self.sparse_pairs is False or self.h % 4 or n_edges > b * v:
+            return False
+        if self.sparse_pairs is True:
+            return True
+        return self.force_generic or self.h not in (128, 256) or v > 128
+
+    @property
+    def sparse(self) -> bool:
+        """Whether the staged batch runs the general path's pair mode."""
+        return self._sparse
 
     @property
     def batch_shape(self):

@@ -90,6 +90,18 @@ enum {
  * k_gru_fwd launches instead of the one-launch fused forward (A/B and tests). */
 #define GGNN_UNFUSED_FWD 32
 
+/* Sparse message passing on the general path ("pair mode", k_pairs.h): the
+ * message transform runs over the (node, channel) pairs with an incoming edge
+ * (X = sum_c (A_c h) W_c + deg beta_c, re-associated) instead of over every
+ * row of every non-empty (graph, channel) tile -- the reference's dependency
+ * trees have ~4 such pairs per node against ~26 non-empty channels per graph
+ * (C = 92).  Same results as the dense loop up to fp32 summation order.
+ * Implies GGNN_GENERIC; needs hidden % 4 == 0 and a batch staged by
+ * ggnn_set_adjacency_edges with num_edges <= b * v (every edge adds at most
+ * 4 pairs, so the pair buffers hold 4 * b * v rows plus channel padding);
+ * ggnn_set_adjacency rejects it. */
+#define GGNN_SPARSE_PAIRS 64
+
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
   int32_t v;     /* vertices per graph       (placeholders['num_vertices']) */

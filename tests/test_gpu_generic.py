@@ -243,3 +243,133 @@ def test_k_gemm_ring_layouts(M, N, K, a_layout, b_layout, precision):
     for got in (ring, old):
         assert np.all(np.abs(got - ref) <= bound), float(np.max(np.abs(got - ref) / bound))
     assert np.all(np.abs(ring - old) <= 2 * bound)
+
+
+# ---------------------------------------------------------------------------
+# Pair mode (GGNN_SPARSE_PAIRS, k_pairs.h): the general path's sparse message
+# passing over the (node, channel) pairs with an incoming edge.
+
+def _trees(b, v, E, seed, extra=0):
+    """Dependency trees with the real label count (E labels -> C = 2E), plus
+    `extra` random extra edges per graph (a head with several children of one
+    label: in-degree > 1 on an outgoing channel)."""
+    rng = np.random.default_rng(seed)
+    pz = 1.0 / np.arange(1, E + 1)
+    pz /= pz.sum()
+    graphs = []
+    for _ in range(b):
+        n = int(rng.integers(max(2, v // 2), v + 1))
+        g = [(int(rng.integers(0, i)), int(rng.choice(E, p=pz)) + 1, i) for i in range(1, n)]
+        g += [(int(rng.integers(0, n)), int(rng.integers(1, E + 1)), int(rng.integers(1, n))) for _ in range(extra)]
+        graphs.append(g)
+    A = np.stack([O.graph_to_adj_mat_bd(g, v, E, dtype=np.float32) for g in graphs])
+    return graphs, A
+
+
+def _run_edges(graphs, v, E, h0, w, T, precision="fp32", dhT=None, sparse="auto", dr=None, force_generic=False):
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    b, h = h0.shape[0], h0.shape[-1]
+    eng = PropagationEngine(h, 2 * E, precision=precision, sparse_pairs=sparse, force_generic=force_generic)
+    dev = eng.device
+    dr = dr or dict(edge_keep=1.0, state_keep=1.0, seed=0)
+    pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}, T=T,
+                            edge_keep=dr["edge_keep"], seed=dr["seed"])
+    eng.set_adjacency_edges(graphs, v, E)
+    out = eng.forward(torch.from_numpy(np.ascontiguousarray(h0)).to(dev), pack, T, training=dhT is not None,
+                      state_keep=dr["state_keep"])
+    res = {"hT": out.cpu().numpy(), "sparse": eng.sparse}
+    if dhT is not None:
+        g = eng.backward(torch.from_numpy(np.ascontiguousarray(dhT)).to(dev))
+        res.update({k: (None if t is None else t.cpu().numpy()) for k, t in g.items()})
+    torch.cuda.synchronize()
+    return res
+
+
+@pytest.mark.parametrize("b,v,h,T,extra,sparse", [
+    (6, 30, 400, 4, 0, "auto"),     # the reference's own configuration (hidden 400, T 4, C 92)
+    (4, 46, 400, 3, 3, "auto"),     # several children of one label: in-degree > 1
+    (3, 150, 128, 2, 0, "auto"),    # v > 128
+    (5, 30, 256, 3, 1, True),       # a fast-path hidden size, forced into pair mode
+    (2, 7, 20, 2, 0, "auto"),       # tiny graphs, hidden not a multiple of 32
+])
+def test_sparse_pairs_fp32_parity(b, v, h, T, extra, sparse):
+    E = 46
+    graphs, A = _trees(b, v, E, seed=v + h, extra=extra)
+    rng = np.random.default_rng(h)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=v)
+    dhT = (rng.standard_normal((b, v, h)) * 2.0 ** -8).astype(np.float32)
+    got = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, sparse=sparse)
+    assert got["sparse"]
+    ref, gref = _ref(A, h0, w, T, dhT)
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+    # the same batch through the dense-tile general path: same math, another order
+    dense = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, sparse=False, force_generic=True)
+    assert not dense["sparse"]
+    assert np.abs(got["hT"] - dense["hT"]).max() <= 1e-5
+    for k in GRADS:
+        assert _nmax(got[k], dense[k]) <= 1e-4, k
+
+
+@pytest.mark.parametrize("ek,sk", [(0.9, 0.9), (0.6, 1.0)])
+def test_sparse_pairs_dropout_fp32_parity(ek, sk):
+    """Edge-weight dropout in pair mode: the masked weight copies in the
+    products and the mask of timestep t applied in the dW product's epilogue
+    (no per-timestep slab), against the oracle's Philox masks."""
+    b, v, h, T, E = 4, 30, 400, 3, 46
+    graphs, A = _trees(b, v, E, seed=7, extra=2)
+    rng = np.random.default_rng(3)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=5)
+    dhT = rng.standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=ek, state_keep=sk, seed=424242)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    got = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr)
+    assert got["sparse"]
+    assert np.abs(got["hT"] - ref).max() <= FP32_TOL
+    for k in GRADS:
+        assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_sparse_pairs_16bit(precision):
+    b, v, h, T, E = 4, 30, 400, 4, 46
+    graphs, A = _trees(b, v, E, seed=11)
+    rng = np.random.default_rng(4)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=6)
+    dhT = rng.standard_normal((b, v, h)).astype(np.float32)
+    ref, gref = _ref(A, h0, w, T, dhT)
+    got = _run_edges(graphs, v, E, h0, w, T, precision=precision, dhT=dhT)
+    assert got["sparse"]
+    assert _nrms(got["hT"], ref) <= 1e-2
+    for k in GRADS:
+        assert _nrms(got[k].reshape(gref[k].shape), gref[k]) <= 1e-2, k
+
+
+def test_sparse_pairs_rejected_for_dense_staging_and_too_many_edges():
+    torch = _torch()
+    import ctypes
+    from ggnn_amd import _lib
+    lib = _lib.load()
+    b, v, h, C = 2, 10, 64, 4
+    d = _lib.dims(b, v, h, C, 1, True, "fp32", sparse_pairs=True)
+    nb = _lib.adjacency_bytes(d)
+    adj = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    A = torch.zeros((b, C, v, v), device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = lib.ggnn_set_adjacency(ctypes.byref(d), ctypes.c_void_p(adj.data_ptr()), ctypes.c_void_p(A.data_ptr()), s)
+    assert rc == -1
+    edges = torch.zeros((b * v + 1, 3), dtype=torch.int32, device="cuda")
+    offs = torch.tensor([0, b * v + 1, b * v + 1], dtype=torch.int32, device="cuda")
+    rc = lib.ggnn_set_adjacency_edges(ctypes.byref(d), ctypes.c_void_p(adj.data_ptr()),
+                                      ctypes.c_void_p(edges.data_ptr()), ctypes.c_void_p(offs.data_ptr()),
+                                      b * v + 1, C // 2, s)
+    assert rc == -2
+    bad = _lib.dims(b, v, 66, C, 1, True, "fp32", sparse_pairs=True)
+    assert lib.ggnn_check_dims(ctypes.byref(bad)) == -2     # hidden % 4 != 0
