@@ -311,7 +311,10 @@ def test_sparse_pairs_fp32_parity(b, v, h, T, extra, sparse):
     assert not dense["sparse"]
     assert np.abs(got["hT"] - dense["hT"]).max() <= 1e-5
     for k in GRADS:
-        assert _nmax(got[k], dense[k]) <= 1e-4, k
+        # (dW_c takes single f16 operands in both, <= 3.7e-4 each vs float64, with
+        # different rounding points: Y = sum of h rows here, h and dM there)
+        tol = FP32_TOL if k in ("edge_weights", "gates_kernel", "candidate_kernel") else 1e-4
+        assert _nmax(got[k], dense[k]) <= tol, k
 
 
 @pytest.mark.parametrize("ek,sk", [(0.9, 0.9), (0.6, 1.0)])
