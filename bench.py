@@ -325,6 +325,20 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10,
     return out
 
 
+def tree_pair_count(graphs, v, E):
+    """(node, channel) pairs with an incoming edge (graph_to_adj_mat_bd's four
+    entries per edge, distinct per receiving row and channel): the rows pair
+    mode (GGNN_SPARSE_PAIRS) runs the message transform over."""
+    pairs = 0
+    for g in graphs:
+        s = set()
+        for src, lab, dst in g:
+            prv = dst - 1 if dst >= 1 else v - 1
+            s.update(((dst, lab - 1), (src, lab - 1 + E), (dst, E - 1), (prv, 2 * E - 1)))
+        pairs += len(s)
+    return pairs
+
+
 def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
     """Side measurement (SURVEY §8f rank 3 / configs[4] shapes): the fwd+bwd
     step on dependency-tree graphs with the real btb label set (std->nivre,
@@ -332,7 +346,10 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
     skipping on (the default) and off (GGNN_DENSE_CHANNELS).  Sentence-sized
     graphs (the real dev set: mean 24.6 nodes; bucket v <= 32),
     n ~ U{v/2..v} nodes, random heads before dependents, Zipf-like labels
-    (P(label k) ~ 1/k: a few labels such as punct/nsubj/det dominate a treebank)."""
+    (P(label k) ~ 1/k: a few labels such as punct/nsubj/det dominate a treebank).
+    both: also the reference's own model (hidden 400, T = 4) on the general
+    path, in pair mode (GGNN_SPARSE_PAIRS, the default for edge-list batches)
+    and with the dense (graph, channel) tiles, each with its algorithmic rate."""
     import torch
     from ggnn_amd.dist import FlatGradients
     from ggnn_amd.engine import PropagationEngine
@@ -345,15 +362,27 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
     for _ in range(b):
         n = int(rng.integers(v // 2, v + 1))
         graphs.append([(int(rng.integers(0, i)), int(rng.choice(E, p=pz)) + 1, i) for i in range(1, n)])
-    occ = [int((O.graph_to_adj_mat_bd(g_, v, E, dtype=np.float32).reshape(C, -1).max(1) > 0).sum()) for g_ in graphs[:16]]
+    occ = [int((O.graph_to_adj_mat_bd(g_, v, E, dtype=np.float32).reshape(C, -1).max(1) > 0).sum()) for g_ in graphs]
+    pairs = tree_pair_count(graphs, v, E)
     w = O.synthetic_weights(h, C, seed=3)
     w_d = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
     h0 = torch.from_numpy(rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)).to(dev)
     dhT = torch.from_numpy(rng.standard_normal((b, v, h)).astype(np.float32)).to(dev)
     res = {"workload": "b=%d dependency trees, v=%d, hidden=%d, E=%d (C=%d), T=%d, fwd+bwd" % (
-        b, v, h, E, C, T), "nonempty_channels_per_graph_mean": float(np.mean(occ))}
-    for skip in ((True, False) if both else (True,)):
-        eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision="fp32", skip_empty_channels=skip)
+        b, v, h, E, C, T), "nonempty_channels_per_graph_mean": float(np.mean(occ)),
+        "pairs_per_node": pairs / float(b * v)}
+    # algorithmic work of the re-associated contraction (per step, fwd + bwd):
+    # MT over the pair rows 2 P h^2 (x3: fwd, dY, dW), GRU 12 N h^2 (x3), the
+    # adjacency sums (gather / scatter of rows) are not MFMA work
+    N = b * v
+    algo = T * (3 * 2 * pairs * h * h + 3 * 12 * N * h * h)
+    variants = (("skip", dict()), ("dense", dict(skip_empty_channels=False))) if both else ()
+    if h not in (128, 256):
+        variants = ()
+    variants += tuple(((("pairs", dict(sparse_pairs=True)), ("tiles", dict(sparse_pairs=False, force_generic=True)))
+                       if h % 4 == 0 and not both else ()))
+    for name, kw in variants:
+        eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision="fp32", **kw)
         eng.set_adjacency_edges(graphs, v, E)
         grads = FlatGradients(h, C, True, device=dev)
         gv = dict(grads.views)
@@ -366,7 +395,11 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
             eng.backward(dhT, gv)
 
         ms = _timed_events(step, steps)
-        res["skip" if skip else "dense"] = {"ms_per_step": ms, "graphs_per_s": b / (ms * 1e-3)}
+        r = {"ms_per_step": ms, "graphs_per_s": b / (ms * 1e-3)}
+        if name in ("pairs", "tiles"):
+            tf = algo / (ms * 1e-3) / 1e12
+            r.update(algorithmic_tflops=tf, frac_of_bf16_peak=tf / BF16_DENSE_PEAK_TFLOPS)
+        res[name] = r
         del eng, grads, gv, out
         torch.cuda.empty_cache()
     if both:
@@ -374,7 +407,12 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
         # the reference's own model on these graphs: hidden_size 400, num_timesteps 4
         # (chem_tensorflow.py:95-96, configs[0] / configs[4]), general path
         r4 = real_density_side(dev, b, v, 400, E, 4, steps, both=False)
-        res["reference_defaults_h400_T4"] = {"workload": r4["workload"], **r4["skip"]}
+        res["reference_defaults_h400_T4"] = {
+            "workload": r4["workload"], **r4["pairs"], "pair_mode": "GGNN_SPARSE_PAIRS",
+            "dense_tiles": r4["tiles"], "pairs_per_node": r4["pairs_per_node"],
+            "algorithmic_work": "T*(3*2*P*h^2 + 3*12*N*h^2), P = (node, channel) pairs with an incoming edge, "
+                                "N = b*v rows (the re-associated contraction; the dense formula of SURVEY §8d "
+                                "counts every (row, channel))"}
     return res
 
 
