@@ -143,7 +143,7 @@ def test_generic_adjacency_from_edges():
     A = np.stack([O.graph_to_adj_mat_bd(g, v, E, dtype=np.float32) for g in graphs])
     h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
     w = O.synthetic_weights(h, 2 * E, seed=1)
-    eng = PropagationEngine(h, 2 * E)
+    eng = PropagationEngine(h, 2 * E, sparse_pairs=False)    # the dense-tile general path
     dev = eng.device
     pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()})
     eng.set_adjacency_edges(graphs, v, E)
@@ -153,6 +153,14 @@ def test_generic_adjacency_from_edges():
     assert np.array_equal(a, d)
     ref, _ = O.forward(A.astype(np.float64), h0.astype(np.float64), _f64(w), T, keep_cache=False)
     assert np.abs(a - ref).max() <= FP32_TOL
+    # the default ("auto") stages this edge-list batch in pair mode: same
+    # math in another summation order
+    pe = PropagationEngine(h, 2 * E)
+    pe.set_adjacency_edges(graphs, v, E)
+    assert pe.sparse
+    p = pe.forward(torch.from_numpy(h0).to(dev), pe.pack_weights(
+        {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}), T).cpu().numpy()
+    assert np.abs(p - ref).max() <= FP32_TOL and np.abs(p - a).max() <= 1e-5
 
 
 def test_generic_bf16_statistical():
