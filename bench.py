@@ -302,6 +302,13 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10,
             fl = kernel_algo_flops(k, b, v, h, C, T)
             d = {"avg_launch_ms": avg, "tflops": fl / (avg * 1e-3) / 1e12,
                  "frac_of_bf16_peak": fl / (avg * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+            if k == "gru_fwd":
+                # SURVEY §8(d)'s algorithmic GRU bytes: X, h in + h' out as fp32
+                # (12 v h b) plus the saved r, u, c (12 v h b) -- the contract's
+                # bytes, not the kernel's own traffic
+                ab = 24 * v * h * b
+                d.update(algorithmic_bytes_per_launch=ab,
+                         frac_of_hbm_peak_algorithmic=ab / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS)
             kt = tr.get("kernels", {}).get(k)
             if kt:
                 # PMC HBM bytes per launch (profiles/pmc_traffic_<precision>.json);

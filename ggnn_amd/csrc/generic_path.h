@@ -68,6 +68,10 @@ struct GenWsL {
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
   size_t hsl(int t) const { return hs + (size_t)t * nh * 4; }
   size_t x(int t) const { return X + (size_t)(t % ns) * nh * 4; }
+  // backward: dzc [T][N][H], dzg [T][N][2H] kept per timestep, so the GRU
+  // weight gradients run once over all T*N rows after the timestep loop
+  size_t dzc(int t) const { return DZC + (size_t)t * nh * 4; }
+  size_t dzg(int t) const { return DZG + (size_t)t * nh * 8; }
   size_t g(int t) const { return G + (size_t)(t % ns) * nh * 8; }
   size_t rh(int t) const { return RH + (size_t)(t % ns) * nh * 4; }
   size_t cc(int t) const { return CC + (size_t)(t % ns) * nh * 4; }
@@ -96,8 +100,8 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
   if (tr) {
     L.Dl = o;  o += a4;
     L.DXH = o; o += 2 * a4;
-    L.DZC = o; o += a4;
-    L.DZG = o; o += 2 * a4;
+    L.DZC = o; o += a4 * c.T;
+    L.DZG = o; o += 2 * a4 * c.T;
     L.DRH = o; o += a4;
     if (c.ed && !c.sparse) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
     L.gmax = o; o += al(4);
@@ -412,8 +416,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
   float* Dl = P<float>(ws, L.Dl);
   float* DXH = P<float>(ws, L.DXH);
-  float* DZC = P<float>(ws, L.DZC);
-  float* DZG = P<float>(ws, L.DZG);
   float* DRH = P<float>(ws, L.DRH);
   float* dM = P<float>(ws, L.M);
   {
@@ -423,11 +425,14 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
                        gmax);
   }
-  // split-K chunk of the weight-gradient products over the N rows
-  const long KC = std::max<long>(256, ((N + 63) / 64 + 31) & ~31L);
-  const int nkc = (int)((N + KC - 1) / KC);
+  // The weight gradients take single f16 operands in the fp32-parity mode, as
+  // the fast path's k_wgrad256 does (measured <= 3.7e-4 normalised against
+  // float64; the dh / dX chain keeps the split limbs): a third of the MFMAs
+  constexpr int WPREC = Prec<PREC>::split ? PREC_F16 : PREC;
   for (int t = c.T - 1; t >= 0; --t) {
     const float* ht = P<float>(ws, L.hsl(t));
+    float* DZC = P<float>(ws, L.dzc(t));
+    float* DZG = P<float>(ws, L.dzg(t));
     const float* G = P<float>(ws, L.g(t));
     // (row slices of the element-wise kernels: ~256 rows each, one bias atomic per column per slice)
     const dim3 ewg((unsigned)((H + 255) / 256), (unsigned)std::max<long>(1, std::min<long>(512, N / 64)));
@@ -458,23 +463,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.M = (int)N; a.N = (int)(2 * H); a.K = (int)(2 * H);
       if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
     }
-    // GRU weight gradients: split-K over row chunks, atomics.  The weight
-    // gradients take single f16 operands in the fp32-parity mode, as the fast
-    // path's k_wgrad256 does (measured <= 3.7e-4 normalised against float64;
-    // the dh / dX chain keeps the split limbs): a third of the MFMAs
-    constexpr int WPREC = Prec<PREC>::split ? PREC_F16 : PREC;
-    auto wg = [&](const float* Aop, const float* Bop, long ldB, int Nn, float* out, long ldO) {
-      GemmArgs a = gg_args();
-      a.A = Aop; a.sAp = KC * H; a.sAm = 1; a.sAk = H;
-      a.B = Bop; a.sBp = KC * ldB; a.sBk = ldB; a.sBn = 1;
-      a.D = out; a.sDm = ldO; a.sDn = 1; a.mode = GG_ATOMIC;
-      a.Z = nkc; a.M = (int)H; a.N = Nn; a.K = (int)KC; a.Ktot = N; a.sKp = KC;
-      return gg_launch<WPREC>(a, false, false, false, K_WGRAD, s);
-    };
-    if (int e = wg(P<float>(ws, L.x(t)), DZC, H, (int)H, dWc, H)) return e;
-    if (int e = wg(P<float>(ws, L.rh(t)), DZC, H, (int)H, dWc + H * H, H)) return e;
-    if (int e = wg(P<float>(ws, L.x(t)), DZG, 2 * H, (int)(2 * H), dWg, 2 * H)) return e;
-    if (int e = wg(ht, DZG, 2 * H, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
     if (c.sparse) {
       // pair mode (k_pairs.h): Y_t recomputed from the saved h_t, dXg = dX
       // of the pair rows, dbeta, dY = dXg W_c^T, dh += A^T dY, dW_c += Y^T dXg
@@ -561,6 +549,29 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       hipLaunchKernelGGL(k_gen_delta, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
                          c.sdrop, t - 1, gmax, t == 0 ? 1 : 0);
     }
+  }
+  // GRU weight gradients over all T*N rows at once: z = (row chunk, timestep),
+  // split-K with fp32 atomics; the chunk count is sized for ~1024 workgroups
+  // per product (fewer atomics than per-timestep launches of the same size)
+  {
+    auto wg = [&](size_t aoff, long slotA, size_t boff, long ldB, long slotB, int Nn, float* out, long ldO) {
+      const long tiles = ((H + 127) / 128) * ((Nn + 127) / 128);
+      const long zt = std::max<long>(1, 1024 / tiles);
+      long KC = ((c.T * N + zt - 1) / zt + 31) & ~31L;
+      KC = std::min<long>(std::max<long>(KC, 256), (N + 31) & ~31L);
+      const int nkc = (int)((N + KC - 1) / KC);
+      GemmArgs a = gg_args();
+      a.A = P<float>(ws, aoff); a.sAp = KC * H; a.sAq = slotA; a.sAm = 1; a.sAk = H;
+      a.B = P<float>(ws, boff); a.sBp = KC * ldB; a.sBq = slotB; a.sBk = ldB; a.sBn = 1;
+      a.D = out; a.sDm = ldO; a.sDn = 1; a.mode = GG_ATOMIC;
+      a.zdiv = c.T; a.Z = nkc * c.T; a.M = (int)H; a.N = Nn; a.K = (int)KC; a.Ktot = N; a.sKp = KC;
+      return gg_launch<WPREC>(a, false, false, false, K_WGRAD, s);
+    };
+    const long sl = (long)L.nh;  // floats between timestep slots of an [N][H] array
+    if (int e = wg(L.x(0), sl, L.dzc(0), H, sl, (int)H, dWc, H)) return e;
+    if (int e = wg(L.rh(0), sl, L.dzc(0), H, sl, (int)H, dWc + H * H, H)) return e;
+    if (int e = wg(L.x(0), sl, L.dzg(0), 2 * H, 2 * sl, (int)(2 * H), dWg, 2 * H)) return e;
+    if (int e = wg(L.hsl(0), sl, L.dzg(0), 2 * H, 2 * sl, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
   }
   {
     Prof p(K_IO, s);

@@ -80,16 +80,77 @@ def results_reshaped_btb(targets, computed_values, mask, num_vertices, output_si
     return np.reshape(m, [-1, 1, v, o]), np.reshape(cv * m, [-1, 1, v, o]), np.reshape(t, [-1, 1, v, o])
 
 
+def _first_max(t, is_probability):
+    """adj_mat_to_target's choice for a batch: t [b, n, K] (node rows 1..v-1,
+    (edge type, source) flattened).  Returns (keep [b, n] bool, first [b, n])."""
+    mx = t.max(axis=2)
+    eq = t == (mx[..., None] if is_probability else 1)
+    return (mx != 0) & eq.any(axis=2), eq.argmax(axis=2)
+
+
 def batch_las_uas(labels, computed_values, num_vertices, mask, labels_e, computed_values_e, mask_edges,
                   output_size, output_size_edges):
     """Mean (LAS, UAS, label accuracy) over a batch, as
     ``humanize_batch_results_btb`` computes them (chem_tensorflow_dense.py:1160-1215,
     without its file output): heads from the arg-max of the head
-    probabilities, labels from the arg-max of the label probabilities."""
+    probabilities, labels from the arg-max of the label probabilities.
+
+    Vectorised over the batch: every graph whose four node lists (target and
+    result heads and labels) keep the same nodes -- the normal case, every
+    real node has a target and a non-zero probability row -- is scored from
+    per-node comparisons; any other graph goes through the reference's
+    list-based path (get_las_uas compares the lists by POSITION).  The
+    per-graph scores are added in graph order, as the reference does, so the
+    result is bit-identical (tests/test_evaluation.py: fixtures of the
+    reference's own functions)."""
     _, res, tgt = results_reshaped_btb(labels, computed_values, mask, num_vertices, output_size,
                                        output_size_edges)
     _, res_e, tgt_e = results_reshaped_btb(labels_e, computed_values_e, mask_edges, num_vertices, output_size,
                                            output_size_edges, is_edge=True)
+    b, v, o = tgt.shape[0], tgt.shape[2], tgt.shape[3]
+    if v < 2:
+        return _batch_las_uas_lists(res, tgt, res_e, tgt_e)
+    # node rows 1..v-1, (edge type, source) flattened: heads [b, v-1, o] (one edge
+    # type), labels [b, v-1, e] (source 0)
+    kt, ft = _first_max(tgt[:, 0, 1:, :], False)
+    kr, fr = _first_max(res[:, 0, 1:, :], True)
+    kte, fte = _first_max(np.transpose(tgt_e[:, :, 1:, 0], (0, 2, 1)), False)
+    kre, fre = _first_max(np.transpose(res_e[:, :, 1:, 0], (0, 2, 1)), True)
+    same = (kt == kr).all(axis=1) & (kt == kte).all(axis=1) & (kt == kre).all(axis=1)
+    n = kt.sum(axis=1)
+    head_ok = (ft == fr) & kt
+    lab_ok = (fte == fre) & kt
+    las_n = (head_ok & lab_ok).sum(axis=1)
+    uas_n = head_ok.sum(axis=1)
+    lab_n = lab_ok.sum(axis=1)
+    acc_las = acc_uas = acc_uas_e = 0.0
+    for i in range(b):
+        if same[i] and n[i] > 0:
+            ni = int(n[i])
+            las, uas, uas_e = int(las_n[i]) / ni, int(uas_n[i]) / ni, int(lab_n[i]) / ni
+        else:
+            las, uas, uas_e = _graph_las_uas(res[i], tgt[i], res_e[i], tgt_e[i])
+        acc_las += las
+        acc_uas += uas
+        acc_uas_e += uas_e
+    return acc_las / b, acc_uas / b, acc_uas_e / b
+
+
+def _graph_las_uas(res, tgt, res_e, tgt_e):
+    """One graph through the reference's lists (chem_tensorflow_dense.py:1179-1199)."""
+    tg_h = adj_mat_to_target(tgt)
+    tg_e = adj_mat_to_target(tgt_e)
+    target_graph = merge_head_and_edge_graph(tg_h, tg_e)
+    rg_h = adj_mat_to_target(res, is_probability=True, true_target=tg_h)
+    rg_e = adj_mat_to_target(res_e, is_probability=True)
+    result_graph = merge_head_and_edge_graph(rg_h, rg_e)
+    las, uas = get_las_uas(target_graph, result_graph)
+    _, uas_e = get_las_uas(tg_e, rg_e, is_edge=True)
+    return las, uas, uas_e
+
+
+def _batch_las_uas_lists(res, tgt, res_e, tgt_e):
+    """batch_las_uas through the reference's per-graph lists only."""
     b = tgt.shape[0]
     acc_las = acc_uas = acc_uas_e = 0.0
     for i in range(b):

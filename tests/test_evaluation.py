@@ -222,3 +222,42 @@ def test_las_uas_equal_the_reference_on_real_dev_batches():
             assert tg == ref["target"] and rg == ref["result"] and rg_e == ref["result_e"], (k, i)
             assert E.get_las_uas(tg, rg) == (ref["las"], ref["uas"])
     assert int(ev["n_batches"]) >= 6
+
+
+def test_batch_las_uas_vectorised_matches_lists():
+    """The vectorised batch scoring against the reference's per-graph list
+    path on random batches with ties, all-zero probability rows (skipped
+    nodes: lists shift by position) and padded nodes -- exact equality."""
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        b, v, o, e = int(rng.integers(1, 6)), int(rng.integers(2, 12)), 12, int(rng.integers(1, 5))
+        o = max(o, v)
+        heads = np.zeros((b, v, o), np.float32)
+        labs = np.zeros((b, v, e), np.float32)
+        mask = np.zeros((b, v, o), np.float32)
+        mask_e = np.zeros((b, v, e), np.float32)
+        for g in range(b):
+            n = int(rng.integers(1, v + 1))
+            for node in range(1, n):
+                heads[g, node, rng.integers(0, n)] = 1
+                labs[g, node, rng.integers(0, e)] = 1
+            mask[g, :n, :n] = 1
+            mask_e[g, :n, :] = 1
+        lv = [2, 5, 255][trial % 3]
+        ph = (rng.integers(0, lv + 1, heads.shape) / lv).astype(np.float32)
+        pe = (rng.integers(0, lv + 1, labs.shape) / lv).astype(np.float32)
+        if trial % 4 == 0:                     # some real nodes with an all-zero row
+            ph[rng.random((b, v)) < 0.2] = 0
+        if trial % 5 == 0:
+            pe[rng.random((b, v)) < 0.2] = 0
+        args = (heads.reshape(b, -1), ph.reshape(b, -1), v, mask.reshape(b, -1), labs.reshape(b, -1),
+                pe.reshape(b, -1), mask_e.reshape(b, -1), o, e)
+        _, res, tgt = E.results_reshaped_btb(args[0], args[1], args[3], v, o, e)
+        _, res_e, tgt_e = E.results_reshaped_btb(args[4], args[5], args[6], v, o, e, is_edge=True)
+        try:
+            ref = E._batch_las_uas_lists(res, tgt, res_e, tgt_e)
+        except ZeroDivisionError:
+            with pytest.raises(ZeroDivisionError):
+                E.batch_las_uas(*args)
+            continue
+        assert E.batch_las_uas(*args) == ref, trial

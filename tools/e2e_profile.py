@@ -1,33 +1,49 @@
-"""cProfile of one run_epoch at the reference's default params (the
-end_to_end_run_epoch side line of bench.py): where the host time goes."""
+"""Where run_epoch's time goes at the reference's default params on its own
+sentences (--train_with_dev): wall time per batch vs the library's kernel
+time per batch (HIP events around every launch), and a cProfile of the host.
+
+    python tools/e2e_profile.py [--no-cprofile]
+"""
 import cProfile
 import os
 import pstats
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from ggnn_amd.batching import synthetic_treebank  # noqa: E402
+from ggnn_amd import _lib  # noqa: E402
+from ggnn_amd.batching import TRAIN_WITH_DEV, wsj_model_sizes  # noqa: E402
 from ggnn_amd.model import DenseGGNNChemModel  # noqa: E402
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
-    raw = synthetic_treebank(1200, seed=2)
-    m = DenseGGNNChemModel(num_edge_types=46, output_size_edges=12, pos_size=46, vocab_size=39549,
-                           params={"compact_adjacency": True}, seed=0, device=dev)
-    train = m.process_raw_graphs(raw[:1000], True)
-    valid = m.process_raw_graphs(raw[1000:], False)
+    np.random.seed(0)
+    m = DenseGGNNChemModel(params={"compact_adjacency": True}, seed=0, device=dev, **wsj_model_sizes())
+    train = m.load_data(TRAIN_WITH_DEV["train_file"], True)
+    valid = m.load_data(TRAIN_WITH_DEV["valid_file"], False)
     m.run_epoch("warm-up", train, True)
-    pr = cProfile.Profile()
-    pr.enable()
-    tr = m.run_epoch("train", train, True)
-    va = m.run_epoch("valid", valid, False)
-    pr.disable()
-    print("train inst/s %.1f  valid inst/s %.1f" % (tr[3], va[3]))
-    st = pstats.Stats(pr)
-    st.sort_stats("cumulative").print_stats(45)
-    st.sort_stats("tottime").print_stats(30)
+    for name, data, tr in (("train", train, True), ("valid", valid, False)):
+        timer = _lib.KernelTimer(max_launches=400000)
+        t0 = time.perf_counter()
+        with timer:
+            r = m.run_epoch(name, data, tr)
+            torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ks = {k: v for k, v in timer.total_ms.items() if v}
+        print("%s: %d batches, %.1f inst/s (timed run: wall %.1f ms/batch, kernels %.2f ms/batch, launches %.0f/batch)"
+              % (name, r[4], r[3], wall * 1e3 / r[4], sum(ks.values()) / r[4],
+                 sum(timer.launches.values()) / r[4]))
+        print("   per kind ms/batch:", {k: round(v / r[4], 3) for k, v in ks.items()})
+    if "--no-cprofile" not in sys.argv:
+        pr = cProfile.Profile()
+        pr.enable()
+        tr = m.run_epoch("train", train, True)
+        pr.disable()
+        print("train inst/s (cProfile on) %.1f" % tr[3])
+        st = pstats.Stats(pr)
+        st.sort_stats("tottime").print_stats(35)
