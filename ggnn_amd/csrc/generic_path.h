@@ -183,8 +183,11 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   if (a.Ktot == 0) a.Ktot = a.K;
   if ((g_gemm_force == 2 || (g_gemm_force == 0 && gemm_kernel_env() == 0)) && ring_ok(a, A16, AKC, BKC)) {
     // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
-    // per-(graph, channel) products of v = 30 sentence graphs), 128 otherwise
-    const bool small = AKC && a.M <= 64 && ring_small_env();
+    // per-(graph, channel) products of v = 30 sentence graphs), and for
+    // products whose 128-row grid would leave most CUs idle (the GRU products
+    // of a 20-sentence batch: M ~ 600 rows -> 5 x 7 tiles); 128 otherwise
+    const long grid128 = (long)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.Z;
+    const bool small = AKC && (a.M <= 64 || grid128 < 128) && ring_small_env();
     const int bm = small ? 32 : 128;
     const int tn = (a.N + 127) / 128, tm = (a.M + bm - 1) / bm;
     const long nwg = (long)tn * tm * a.Z;

@@ -591,7 +591,7 @@ class DenseGGNNChemModel(BtbBatching):
         if dev[0].device.type != "cuda":
             p["host"], p["event"] = [t.cpu() for t in dev], None
             return p
-        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in dev]
+        host = [self._pinned(i, t) for i, t in enumerate(dev)]
         for h, t in zip(host, dev):
             h.copy_(t, non_blocking=True)
         ev = torch.cuda.Event()
@@ -599,12 +599,30 @@ class DenseGGNNChemModel(BtbBatching):
         p["host"], p["event"] = host, ev
         return p
 
+    def _pinned(self, slot, t):
+        """A page-locked host tensor shaped like device tensor t for fetch slot
+        `slot`, from a small pool (a pinned allocation per batch cost more than
+        the copy).  Two sets alternate: run_epoch keeps one batch in flight."""
+        pool = self.__dict__.setdefault("_pin_pool", {})
+        self._pin_flip = getattr(self, "_pin_flip", 0)
+        key = (slot, self._pin_flip)
+        buf = pool.get(key)
+        n = t.numel()
+        if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+            buf = torch.empty(max(n, 1), dtype=t.dtype, pin_memory=True)
+            pool[key] = buf
+        if slot == 2:
+            self._pin_flip ^= 1       # the last fetch of a batch: the next batch takes the other set
+        return buf[:n].view(t.shape)
+
     def _finish_batch(self, p):
         """(loss, _score_arrays(...)) of a batch queued by _fetch_batch."""
         if p["event"] is not None:
             p["event"].synchronize()
         hl, hp, hpe = p["host"]
-        return float(hl), self._score_arrays(p["ph"], hp.numpy(), hpe.numpy())
+        # (copies: the pinned buffers are reused two batches later, and run_epoch
+        # keeps the probabilities in its returned lists)
+        return float(hl.sum()), self._score_arrays(p["ph"], hp.numpy().copy(), hpe.numpy().copy())
 
     # the reference's per-task "chemical accuracy" normalisers (chem_tensorflow.py:529-531)
     CHEMICAL_ACCURACIES = np.array([0.066513725, 0.012235489, 0.071939046, 0.033730778, 0.033486113, 0.004278493,
