@@ -40,10 +40,11 @@ if __name__ == "__main__":
                  sum(timer.launches.values()) / r[4]))
         print("   per kind ms/batch:", {k: round(v / r[4], 3) for k, v in ks.items()})
     if "--no-cprofile" not in sys.argv:
-        pr = cProfile.Profile()
-        pr.enable()
-        tr = m.run_epoch("train", train, True)
-        pr.disable()
-        print("train inst/s (cProfile on) %.1f" % tr[3])
-        st = pstats.Stats(pr)
-        st.sort_stats("tottime").print_stats(35)
+        for name, data, tr_ in (("train", train, True), ("valid", valid, False)):
+            pr = cProfile.Profile()
+            pr.enable()
+            r = m.run_epoch(name, data, tr_)
+            pr.disable()
+            print("%s inst/s (cProfile on) %.1f" % (name, r[3]))
+            st = pstats.Stats(pr)
+            st.sort_stats("tottime").print_stats(30)
