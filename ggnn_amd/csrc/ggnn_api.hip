@@ -189,7 +189,7 @@ PackL pack_layout(const Cfg& c) {
 
 // ---- staged adjacency
 struct AdjL {
-  size_t Ab, AbT, deg, chl, chl_all, extt, ext, total;
+  size_t Ab, AbT, deg, chl, chl_all, total;
 };
 AdjL adj_layout(const Cfg& c) {
   AdjL L;
@@ -199,8 +199,6 @@ AdjL adj_layout(const Cfg& c) {
   L.deg = o; o += al((size_t)c.b * c.C * c.V * 2);
   L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);  // per-graph non-empty channel lists (k_chan_list)
   L.chl_all = o; o += al((size_t)(c.C + 1) * 4);     // identity list (dense channel loop)
-  L.extt = o; o += al((size_t)c.b * c.C * 2);         // per-tile active extent (k_prep_adj / k_adj_deg)
-  L.ext = o;  o += al((size_t)c.b * 4);               // per-graph active extent (k_chan_list)
   L.total = o;
   return L;
 }
@@ -257,16 +255,13 @@ template <typename T> const T* P(const void* base, size_t off) { return (const T
 // the channel list the compute kernels loop over: per-graph non-empty
 // channels (graph stride C+1), or the identity list (stride 0) under
 // GGNN_DENSE_CHANNELS
-// ext: the per-graph active extents (k_chan_list), or null (every row block)
-// under GGNN_DENSE_CHANNELS, which turns off all exact-zero skipping
 struct ChanL {
   const int* p;
   int stride;
-  const int* ext;
 };
 ChanL chan_lists(const Cfg& c, const void* adj, const AdjL& AL) {
-  if (c.flags & GGNN_DENSE_CHANNELS) return ChanL{P<int>(adj, AL.chl_all), 0, nullptr};
-  return ChanL{P<int>(adj, AL.chl), c.C + 1, P<int>(adj, AL.ext)};
+  if (c.flags & GGNN_DENSE_CHANNELS) return ChanL{P<int>(adj, AL.chl_all), 0};
+  return ChanL{P<int>(adj, AL.chl), c.C + 1};
 }
 int grid1d(long n, int bs = 256) {
   const long g = (n + bs - 1) / bs;
@@ -287,7 +282,7 @@ void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, ChanL c
                      const void* pk, void* Xa, void* XT, hipStream_t s) {
   Prof p(K_PROP_FWD, s);
   hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab, chl.p, chl.stride,
-                     chl.ext, P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
+                     P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, ChanL chl,
@@ -295,7 +290,7 @@ void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const
                      const uint32_t* gmax, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg, chl.p,
-                     chl.stride, chl.ext,
+                     chl.stride,
                      P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1,
                      gmax);
 }
@@ -420,7 +415,6 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     const ChanL cl = chan_lists(c, adj, AL);
     fa.chl = cl.p;
     fa.chs = cl.stride;
-    fa.ext = cl.ext;
     fa.Wp = P<u16>(pack, PL.wf(0));
     fa.wlo = PL.loW;
     fa.wstep = c.ed ? (long)(PL.szW / 2) : 0;
@@ -916,10 +910,9 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
       hipLaunchKernelGGL((k_adj_from_edges<VV, F>), dim3(grid), dim3(256), 0, s, edges, graph_offsets, c.b,      \
                          c.vin, num_edge_types, P<u16>(adj, L.Ab), P<u16>(adj, L.AbT));                           \
     hipLaunchKernelGGL((k_adj_deg<VV, F>), dim3((unsigned)tiles), dim3(VV), 0, s, P<const u16>(adj, L.Ab),        \
-                       P<const u16>(adj, L.AbT), P<u16>(adj, L.deg), P<u16>(adj, L.extt));                       \
-    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg),                    \
-                       P<const u16>(adj, L.extt), c.C, P<int>(adj, L.chl), P<int>(adj, L.chl_all),               \
-                       P<int>(adj, L.ext));                                                                      \
+                       P<u16>(adj, L.deg));                                                                      \
+    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,               \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                              \
   } while (0)
   const bool f16 = c.prec != PREC_BF16;
   if (c.V == 32) { if (f16) ADJ_EDGES(32, true); else ADJ_EDGES(32, false); }
@@ -948,10 +941,9 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
 #define PREP_ADJ(VV, F)                                                                                       \
   do {                                                                                                        \
     hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab),                 \
-                       P<u16>(adj, L.AbT), P<u16>(adj, L.deg), P<u16>(adj, L.extt));                          \
-    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg),                  \
-                       P<const u16>(adj, L.extt), c.C, P<int>(adj, L.chl), P<int>(adj, L.chl_all),             \
-                       P<int>(adj, L.ext));                                                                   \
+                       P<u16>(adj, L.AbT), P<u16>(adj, L.deg));                                               \
+    hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,             \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                           \
   } while (0)
   if (c.prec != PREC_BF16) {
     if (c.V == 32) PREP_ADJ(32, true);

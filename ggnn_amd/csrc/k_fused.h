@@ -35,7 +35,6 @@ struct FusedFwdArgs {
   const u16* Ab;                // staged adjacency [b][C][128][128] (k_prep.h layout)
   const int* chl;               // per-graph non-empty channel lists (k_chan_list), graph stride chs
   int chs;                      //   (0: the identity list, dense channel loop)
-  const int* ext;               // per-graph active extents (k_chan_list), or null: every row block
   const u16* Wp;                // packed edge weights, hi part; lo at +wlo elements
   long wlo, wstep;              // wstep: elements between per-timestep copies (edge dropout), else 0
   const float* beta;            // [C][H]
@@ -91,9 +90,6 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
   const int* cl = a.chl + (long)g * a.chs;
   const int nc = cl[0];
   auto chan = [&](int i) { return cl[1 + i]; };
-  // 32-row blocks up to the graph's active extent: past it the messages and
-  // aggregates are exact zeros (k_prop_fwd); the GRU still runs on every row
-  const int nb = a.ext ? min(VT, (a.ext[g] + 31) >> 5) : VT;
   float* xs = a.Xs + row0 * H;
   const rsrc_t rxs = mkrsrc(xs, R * H * 4);
   const rsrc_t wgh = mkrsrc(a.Wgp, 4 * H * H * 2), wgl = mkrsrc(a.Wgp + a.wlo_g, 4 * H * H * 2);
@@ -165,7 +161,6 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       b_pipeline<KS, 2>(ldw, [&](int ks, const F2& w) {
 #pragma unroll
         for (int rt = 0; rt < VT; ++rt) {
-          if (rt >= nb) continue;
           const int off = koff(rt * 32 + l32, 2 * ks + hh);
           const frag ah = lds_frag(img_hi, off);
           mma<PREC>(accm[rt], ah, SPLIT ? lds_frag(img_lo, off) : ah, w.a, w.b);
@@ -174,12 +169,10 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       __syncthreads();  // S1: A_c visible
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
-        if (rt >= nb) continue;
         const frag mh0 = acc_hi<F16>(accm[rt], 0), mh1 = acc_hi<F16>(accm[rt], 1);
         const frag ml0 = SPLIT ? acc_lo<true>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<true>(accm[rt], 1) : mh1;
 #pragma unroll
         for (int it = 0; it < VT; ++it) {
-          if (it >= nb) continue;
           const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
           const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
           mma_xa<PREC>(accx[it], a0, mh0, ml0);

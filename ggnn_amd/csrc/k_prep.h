@@ -50,18 +50,12 @@ __global__ void k_copy_f32(const float* __restrict__ s, float* __restrict__ d, l
 //   AbT [V][V] bf16 = A^T, natural order (B operand of k_prop_bwd);
 //   deg [V] 16-bit limbs = row sums (in-degree per channel, <= 128: exact),
 //       the B operand of k_prop_bwd's dL/dbeta product.
-//   extt[tile] = the tile's active extent: 1 + the largest node index with an
-//       edge on either side (0 for an empty tile; k_chan_list turns it into the
-//       graph's extent, below which the padded tail's rows are skipped)
 template <int V, bool F16>
 __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, int vin,
                                                   u16* __restrict__ Ab, u16* __restrict__ AbT,
-                                                  u16* __restrict__ deg, u16* __restrict__ extt) {
+                                                  u16* __restrict__ deg) {
   constexpr int P = V + 8;           // row pitch (u16): 16-B aligned rows, odd dword pitch / 4
   __shared__ __attribute__((aligned(16))) u16 tt[V][P];  // A[j][i] (transposed)
-  __shared__ int s_ext;
-  if (threadIdx.x == 0) s_ext = 0;
-  int ext = 0;
   const long tile = blockIdx.x;  // g*C + c
   const float* src = A + tile * (long)vin * vin;
   u16* ab = Ab + tile * V * V;
@@ -128,21 +122,13 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
         for (int r = 0; r < 4; ++r) rs[r] += __shfl_xor(rs[r], o);
       if (act && sl == 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          deg[tile * V + i + r] = to_limb<F16>(rs[r]);
-          if (rs[r] != 0.f) ext = max(ext, i + r + 1);  // a receiving row
-        }
+        for (int r = 0; r < 4; ++r) deg[tile * V + i + r] = to_limb<F16>(rs[r]);
     }
     __syncthreads();
     for (int q = threadIdx.x; q < V * V / 8; q += 256) {
       const int i = q / (V / 8), p = (q % (V / 8)) * 8;
-      const uint4 x = *(const uint4*)&tt[i][p];
-      *(uint4*)(at + i * V + p) = x;
-      if (x.x | x.y | x.z | x.w) ext = max(ext, i + 1);  // a sending column
+      *(uint4*)(at + i * V + p) = *(const uint4*)&tt[i][p];
     }
-    atomicMax(&s_ext, ext);
-    __syncthreads();
-    if (threadIdx.x == 0) extt[tile] = (u16)s_ext;
     return;
   }
   // padded graphs (vin < V): element-wise, Ab's permuted column order
@@ -158,19 +144,13 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
   __syncthreads();
   for (int q = threadIdx.x; q < V * V / 8; q += 256) {
     const int i = q / (V / 8), p = (q % (V / 8)) * 8;
-    const uint4 x = *(const uint4*)&tt[i][p];
-    *(uint4*)(at + i * V + p) = x;
-    if (x.x | x.y | x.z | x.w) ext = max(ext, i + 1);
+    *(uint4*)(at + i * V + p) = *(const uint4*)&tt[i][p];
   }
   if (threadIdx.x < V) {
     float s = 0.f;
     for (int j = 0; j < V; ++j) s += from_limb<F16>(tt[j][threadIdx.x]);
     deg[tile * V + threadIdx.x] = to_limb<F16>(s);
-    if (s != 0.f) ext = max(ext, (int)threadIdx.x + 1);
   }
-  atomicMax(&s_ext, ext);
-  __syncthreads();
-  if (threadIdx.x == 0) extt[tile] = (u16)s_ext;
 }
 
 // h0 [b][vin][H] fp32 -> hf [N][H] fp32 (pad rows zero) and optional hb in
@@ -370,31 +350,19 @@ __global__ void k_adj_from_edges(const int* __restrict__ edges, const int* __res
   }
 }
 
-// deg[tile][i] = row sums of the staged adjacency (after k_adj_from_edges),
-// extt[tile] = the tile's active extent (as k_prep_adj)
+// deg[tile][i] = row sums of the staged adjacency (after k_adj_from_edges)
 template <int V, bool F16>
-__global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, const u16* __restrict__ AbT,
-                                               u16* __restrict__ deg, u16* __restrict__ extt) {
-  __shared__ int s_ext;
-  if (threadIdx.x == 0) s_ext = 0;
-  __syncthreads();
+__global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, u16* __restrict__ deg) {
   const long tile = blockIdx.x;
   const u16* row = Ab + (tile * V + threadIdx.x) * V;
-  const u16* col = AbT + (tile * V + threadIdx.x) * V;
   float s = 0.f;
-  uint32_t any = 0;
   for (int j = 0; j < V; j += 8) {
     const uint4 x = *(const uint4*)(row + j);
-    const uint4 y = *(const uint4*)(col + j);
-    any |= y.x | y.y | y.z | y.w;
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) s += from_limb<F16>((u16)(w[k] & 0xFFFF)) + from_limb<F16>((u16)(w[k] >> 16));
   }
   deg[tile * V + threadIdx.x] = to_limb<F16>(s);
-  if (s != 0.f || any) atomicMax(&s_ext, (int)threadIdx.x + 1);
-  __syncthreads();
-  if (threadIdx.x == 0) extt[tile] = (u16)s_ext;
 }
 
 // ---- per-graph list of non-empty channels (about 60 % of
@@ -404,23 +372,11 @@ __global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, const
 #define CHL_MAXC 4096
 // Block 0 also writes the identity list [C, 0, 1, .., C-1] at chl_all (the
 // dense channel loop, GGNN_DENSE_CHANNELS: read with graph stride 0).
-// ext[g] = the graph's active extent: 1 + the largest node index with an
-// edge on any channel (max of the tiles' extt).  Rows and columns at or past
-// it hold no edge, so the message transform and aggregation skip the 32-row
-// blocks there exactly (their contributions are exact zeros): the padded tail
-// of a bucketed batch (chem_tensorflow_dense.py:584-585, 877-882).
 template <int V>
-__global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, const u16* __restrict__ extt, int C,
-                                                   int* __restrict__ chl, int* __restrict__ chl_all,
-                                                   int* __restrict__ ext) {
+__global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, int C, int* __restrict__ chl,
+                                                   int* __restrict__ chl_all) {
   __shared__ unsigned char fl[CHL_MAXC];
-  __shared__ int s_ext;
-  if (threadIdx.x == 0) s_ext = 0;
-  __syncthreads();
   const int g = blockIdx.x;
-  int e = 0;
-  for (int c = threadIdx.x; c < C; c += 256) e = max(e, (int)extt[(long)g * C + c]);
-  atomicMax(&s_ext, e);
   if (g == 0) {
     for (int c = threadIdx.x; c < C; c += 256) chl_all[1 + c] = c;
     if (threadIdx.x == 0) chl_all[0] = C;
@@ -442,7 +398,6 @@ __global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, 
     for (int c = 0; c < C; ++c)
       if (fl[c]) out[1 + n++] = c;
     out[0] = n;
-    ext[g] = s_ext;
   }
 }
 

@@ -33,7 +33,7 @@
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, const int* __restrict__ chl, int chs,
-           const int* __restrict__ ext, const u16* __restrict__ Wp, long wlo,
+           const u16* __restrict__ Wp, long wlo,
            const float* __restrict__ beta, ActT<PREC>* __restrict__ Xo, u16* __restrict__ XT, int C, long N) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
@@ -62,10 +62,6 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
   const int* cl = chl + (long)g * chs;
   const int nc = cl[0];
   auto chan = [&](int i) { return cl[1 + i]; };
-  // 32-row blocks up to the graph's active extent (k_chan_list): rows and
-  // columns past it hold no edge, so their messages and aggregates are exact
-  // zeros (the padded tail of a bucketed graph)
-  const int nb = ext ? min(VT, (ext[g] + 31) >> 5) : VT;
 
   stage_rows_k<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
@@ -91,7 +87,6 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     auto mt = [&](int ks, const F2& w) {
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
-        if (rt >= nb) continue;
         const int off = kimg<V>(rt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(h_hi, off);
         const frag al = SPLIT ? lds_frag(h_lo, off) : ah;
@@ -108,12 +103,10 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
     for (int rt = 0; rt < VT; ++rt) {
-      if (rt >= nb) continue;
       const frag mh0 = acc_hi<F16>(accm[rt], 0), mh1 = acc_hi<F16>(accm[rt], 1);
       const frag ml0 = SPLIT ? acc_lo<F16>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<F16>(accm[rt], 1) : mh1;
 #pragma unroll
       for (int it = 0; it < VT; ++it) {
-        if (it >= nb) continue;
         const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
         const frag a1 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + 2 + hh));
         mma_xa<PREC>(accx[it], a0, mh0, ml0);
@@ -170,8 +163,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 template <int V, int H, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
-           const int* __restrict__ chl, int chs, const int* __restrict__ ext, const u16* __restrict__ WTp, long wlo,
-           const float* __restrict__ dh_in, float* __restrict__ dh_out,
+           const int* __restrict__ chl, int chs, const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
            u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
            const uint32_t* __restrict__ gmax) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -219,10 +211,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   const int* cl = chl + (long)g * chs;
   const int nc = cl[0];
   auto chan = [&](int i) { return cl[1 + i]; };
-  // the graph's active 32-row blocks (k_prop_fwd): past them A has no entry,
-  // so dM rows there are exact zeros (still stored for the weight gradients)
-  // and their dh gets no message term
-  const int nb = ext ? min(VT, (ext[g] + 31) >> 5) : VT;
   const u16* ag = AbT + (long)g * C * V * V;
   if (nc > 0) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf, ag + (long)chan(0) * V * V, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
@@ -241,13 +229,10 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
 #pragma unroll
     for (int jt = 0; jt < VT; ++jt) {
       f32x16 am = splat(0.f);
-      if (jt < nb) {
 #pragma unroll
-        for (int s = 0; s < KV; ++s) {
-          if (s >= 2 * nb) continue;  // receivers past the extent: zero A rows
-          const frag b = lds_frag(abuf, SA::off(jt * 32 + l32, 2 * s + hh));
-          mma_xb<PREC>(am, dxh[s], dxl[s], b);
-        }
+      for (int s = 0; s < KV; ++s) {
+        const frag b = lds_frag(abuf, SA::off(jt * 32 + l32, 2 * s + hh));
+        mma_xb<PREC>(am, dxh[s], dxl[s], b);
       }
       const int j = jt * 32 + l32;
 #pragma unroll
@@ -270,7 +255,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       f32x16 db = splat(0.f);
 #pragma unroll
       for (int ss = 0; ss < KV; ++ss) {
-        if (ss >= 2 * nb) continue;  // deg is zero past the extent
         const uint4 d0 = dg[2 * ss], d1 = dg[2 * ss + 1];
         mma_xb<PREC>(db, dxh[ss], dxl[ss], hh ? d1 : d0);
       }
@@ -290,7 +274,6 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     auto pb = [&](int ks, const F2& w) {
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt) {
-        if (jt >= nb) continue;
         const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(m_hi, off);
         const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
