@@ -523,6 +523,8 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side measurements (front-end/heads, bf16 mode)")
+    ap.add_argument("--e2e-only", action="store_true",
+                    help="of the side measurements, only the reference's run_epoch line (every rank; rehearsal)")
     ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (default nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -671,6 +673,8 @@ def main():
     # the reference's own end-to-end run_epoch on its sentences: every rank
     # (data-parallel when world > 1), before the rank-0-only side lines
     e2e = end_to_end_side(dev, rank, world, restrict=(world == 1)) if not args.no_side else None
+    if args.e2e_only:
+        args.no_side = True
     feed_cmp = adjacency_feed_costs(eng, b, v, CFG["e"], dev) if rank == 0 else None
     callers = callers_side(dev, b, v, h) if rank == 0 and not args.no_side else None
     host_slice = (A[:2], h0[:2], w)

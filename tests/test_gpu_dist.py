@@ -101,6 +101,25 @@ def test_two_rank_btb_train_step_equals_union_batch(tmp_path, hidden):
     assert 0 <= tr_las <= tr_uas <= 1 and 0 <= va_las <= va_uas <= 1
 
 
+def test_bench_two_ranks_run_epoch_rehearsal():
+    """bench.py's N-rank run_epoch line (the reference's own metric on its
+    sentences, data parallel over every rank) under torch.distributed.run,
+    2 ranks, gloo on the one GPU: what the driver's 8-GPU run executes."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--e2e-only", "--dist-backend", "gloo"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    e2e = json.loads(lines[0])["end_to_end_run_epoch"]
+    assert e2e["n_ranks"] == 2
+    ep = e2e["epochs"][-1]
+    assert ep["train_instances_per_sec"] > 0 and ep["valid_instances_per_sec"] > 0
+    assert 0 < ep["valid_las"] <= ep["valid_uas"] <= 1 and ep["train_steps"] > 0
+
+
 def test_bench_two_ranks_rehearsal():
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
