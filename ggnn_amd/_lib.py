@@ -19,6 +19,7 @@ GGNN_DENSE_CHANNELS = 8
 GGNN_GENERIC = 16
 GGNN_UNFUSED_FWD = 32
 GGNN_SPARSE_PAIRS = 64
+GGNN_SEED_DEVICE = 128
 PRECISIONS = ("bf16", "fp16", "fp32")
 
 # Every symbol include/ggnn.h declares (checked by tests/test_lib.py).
@@ -29,6 +30,7 @@ EXPORTED = (
     "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_heads_workspace_bytes",
     "ggnn_heads_forward", "ggnn_heads_backward", "ggnn_dbg_gemm", "ggnn_dbg_gemm_ex",
+    "ggnn_adam_step_dev", "ggnn_heads_forward_dev", "ggnn_heads_backward_dev",
 )
 NUM_KERNEL_KINDS = 11
 
@@ -91,6 +93,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_adam_step.restype = _I
         lib.ggnn_adam_step.argtypes = [_P, _I, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                        ctypes.c_float, ctypes.c_int64, ctypes.c_float, _P, _P]
+        lib.ggnn_adam_step_dev.restype = _I
+        lib.ggnn_adam_step_dev.argtypes = [_P, _I, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_float, _P, ctypes.c_float, _P, _P]
         lib.ggnn_dropout_mask.restype = _I
         lib.ggnn_dropout_mask.argtypes = [_DP, _I, _I, _P, _P]
         U64, F = ctypes.c_uint64, ctypes.c_float
@@ -104,6 +109,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_heads_forward.argtypes = [_DP, _P, _I, _P, _P, F, U64, F, _P, _P, _P]
         lib.ggnn_heads_backward.restype = _I
         lib.ggnn_heads_backward.argtypes = [_DP, _P, _I, _P, _P, F, _P, _P, _P, _P, _P]
+        lib.ggnn_heads_forward_dev.restype = _I
+        lib.ggnn_heads_forward_dev.argtypes = [_DP, _P, _I, _P, _P, F, U64, _P, _P, _P, _P]
+        lib.ggnn_heads_backward_dev.restype = _I
+        lib.ggnn_heads_backward_dev.argtypes = [_DP, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]
         lib.ggnn_dbg_gemm.restype = _I
         lib.ggnn_dbg_gemm.argtypes = [_DP, _I, _I, _I, _P, _P, _P, _P]
         lib.ggnn_dbg_gemm_ex.restype = _I
@@ -127,7 +136,9 @@ def check(rc: int, what: str) -> None:
 def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, precision: str = "fp32",
          edge_keep: float = 1.0, state_keep: float = 1.0, seed: int = 0,
          skip_empty_channels: bool = True, force_generic: bool = False,
-         unfused_forward: bool = False, sparse_pairs: bool = False) -> GGNNDims:
+         unfused_forward: bool = False, sparse_pairs: bool = False, seed_device: bool = False) -> GGNNDims:
+    """seed_device: ``seed`` is the address of a device uint64 the kernels read
+    (GGNN_SEED_DEVICE, for hipGraph capture)."""
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s" % (PRECISIONS,))
     flags = (GGNN_USE_EDGE_BIAS if use_edge_bias else 0) | {"bf16": 0, "fp16": GGNN_FP16, "fp32": GGNN_FP32_PARITY}[precision]
@@ -139,6 +150,8 @@ def dims(b: int, v: int, h: int, C: int, T: int, use_edge_bias: bool = True, pre
         flags |= GGNN_UNFUSED_FWD
     if sparse_pairs:
         flags |= GGNN_SPARSE_PAIRS
+    if seed_device:
+        flags |= GGNN_SEED_DEVICE
     return GGNNDims(int(b), int(v), int(h), int(C), int(T), flags, float(edge_keep), float(state_keep),
                     int(seed) & 0xFFFFFFFFFFFFFFFF)
 

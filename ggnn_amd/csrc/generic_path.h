@@ -194,7 +194,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     if (nwg > 0x7fffffffL) return fail(GGNN_EINVAL, "k_gemm_ring: grid too large");
     const dim3 grid((unsigned)nwg);
     Prof p(kind, s);
-    const bool sc = a.scA != 1.0f || a.scB != 1.0f;
+    const bool sc = a.scA != 1.0f || a.scB != 1.0f || a.snum;
 #define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
     if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
@@ -249,9 +249,9 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
                             hipStream_t s) {
   const GenAdjL L = gen_adj_layout(c);
   Prof p(K_ADJ, s);
-  HIPCHK(hipMemsetAsync(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s));
-  HIPCHK(hipMemsetAsync(P<u16>(adj, L.AgT), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s));
-  HIPCHK(hipMemsetAsync(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C, s));
+  fill_async(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s);
+  fill_async(P<u16>(adj, L.AgT), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s);
+  fill_async(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C, s);
   if (ne > 0)
     hipLaunchKernelGGL(k_gen_adj_edges, dim3((unsigned)std::min(c.b, 4096)), dim3(256), 0, s, edges, goff, c.b, c.vin,
                        L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<u16>(adj, L.AgT),
@@ -266,8 +266,8 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
     hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
                        P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
                        P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask));
-    HIPCHK(hipMemsetAsync(P<int>(adj, L.prow), 0xFF, (size_t)c.pcap * 4, s));
-    HIPCHK(hipMemsetAsync(P<float>(adj, L.pdeg), 0, (size_t)c.pcap * 4, s));
+    fill_async(P<int>(adj, L.prow), 0xFF, (size_t)c.pcap * 4, s);
+    fill_async(P<float>(adj, L.pdeg), 0, (size_t)c.pcap * 4, s);
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
                        P<int>(adj, L.prow), P<float>(adj, L.pdeg));
@@ -319,7 +319,7 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
   gen_lists(c, adj, s);
   {
     Prof p(K_IO, s);
-    HIPCHK(hipMemcpyAsync(P<float>(ws, L.hsl(0)), h0, (size_t)N * H * 4, hipMemcpyDeviceToDevice, s));
+    copy_async(P<float>(ws, L.hsl(0)), h0, N * H, s);
   }
   const float* beta = (c.flags & GGNN_USE_EDGE_BIAS) ? P<float>(pack, PL.beta) : nullptr;
   for (int t = 0; t < c.T; ++t) {
@@ -531,7 +531,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     {
       float* G_out = c.ed ? P<float>(ws, L.GW) : dW;
       const bool chunked = AL.nch > 1;
-      if (chunked && c.ed) HIPCHK(hipMemsetAsync(G_out, 0, (size_t)C * H * H * 4, s));
+      if (chunked && c.ed) fill_async(G_out, 0, (size_t)C * H * H * 4, s);
       GemmArgs a = gg_args();
       a.A = ht; a.sAq = v * H; a.sAm = 1; a.sAk = H;
       a.B = dM; a.sBp = v * H; a.sBq = C * v * H; a.sBk = H; a.sBn = 1;

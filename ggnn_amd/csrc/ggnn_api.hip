@@ -63,6 +63,9 @@ struct Prof {
   hipStream_t s;
   Prof(int k, hipStream_t st) : s(st) {
     if (k >= 0 && g_prof.on && g_prof.used < g_prof.cap) {
+      // (no records inside a hipGraph capture: the events would time the capture)
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
       idx = g_prof.used++;
       g_prof.kind[idx] = k;
       hipEventRecord(g_prof.ev[2 * idx], s);
@@ -88,10 +91,13 @@ struct Cfg {
   long pcap;          // pair-row capacity (sparse): 4 * b * v + PAIR_TILE * C, a multiple of PAIR_TILE
 };
 
-Drop make_drop(float keep, uint64_t seed) {
+// seed_ptr (GGNN_SEED_DEVICE): `seed` is the address of a device uint64 read
+// by the kernels at run time
+Drop make_drop(float keep, uint64_t seed, bool seed_ptr = false) {
   Drop d;
-  d.k0 = (uint32_t)seed;
-  d.k1 = (uint32_t)(seed >> 32);
+  d.kp = seed_ptr ? (const uint32_t*)(uintptr_t)seed : nullptr;
+  d.k0 = seed_ptr ? 0u : (uint32_t)seed;
+  d.k1 = seed_ptr ? 0u : (uint32_t)(seed >> 32);
   if (keep >= 1.0f) {
     d.thr = 0;
     d.scale = 1.0f;
@@ -110,7 +116,7 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   if (d->b < 1 || d->v < 1 || d->C < 1 || d->T < 1) return fail(GGNN_EINVAL, "dims: b, v, C, T must be >= 1");
   if (d->h < 1 || d->h > 4096) return fail(GGNN_EUNSUP, "hidden size must lie in 1..4096 (got " + std::to_string(d->h) + ")");
   if (d->flags & ~(GGNN_USE_EDGE_BIAS | GGNN_FP32_PARITY | GGNN_FP16 | GGNN_DENSE_CHANNELS | GGNN_GENERIC |
-                   GGNN_UNFUSED_FWD | GGNN_SPARSE_PAIRS))
+                   GGNN_UNFUSED_FWD | GGNN_SPARSE_PAIRS | GGNN_SEED_DEVICE))
     return fail(GGNN_EINVAL, "unknown flag bits");
   // the specialised kernels: hidden 128 / 256, v <= 128; everything else runs
   // the general path (generic_path.h); pair mode is part of it
@@ -131,8 +137,11 @@ int make_cfg(const ggnn_dims* d, Cfg* c) {
   if (!(d->edge_keep > 0.0f && d->edge_keep <= 1.0f) || !(d->state_keep > 0.0f && d->state_keep <= 1.0f))
     return fail(GGNN_EINVAL, "dropout keep probabilities must lie in (0, 1] (edge_keep " +
                                  std::to_string(d->edge_keep) + ", state_keep " + std::to_string(d->state_keep) + ")");
-  c->edrop = make_drop(d->edge_keep, d->seed);
-  c->sdrop = make_drop(d->state_keep, d->seed);
+  const bool sp = (d->flags & GGNN_SEED_DEVICE) != 0;
+  if (sp && !d->seed && (d->edge_keep < 1.0f || d->state_keep < 1.0f))
+    return fail(GGNN_EINVAL, "GGNN_SEED_DEVICE with dropout needs a device seed address in dims.seed");
+  c->edrop = make_drop(d->edge_keep, d->seed, sp);
+  c->sdrop = make_drop(d->state_keep, d->seed, sp);
   c->ed = c->edrop.thr != 0;
   c->sd = c->sdrop.thr != 0;
   if (!c->generic && (double)c->N * c->H * 4 >= 2147483647.0)
@@ -266,6 +275,16 @@ ChanL chan_lists(const Cfg& c, const void* adj, const AdjL& AL) {
 int grid1d(long n, int bs = 256) {
   const long g = (n + bs - 1) / bs;
   return (int)std::min<long>(std::max<long>(g, 1), 8192);
+}
+// device-side fill / copy on the stream (kernels: capture-safe, see k_fill)
+void fill_async(void* p, unsigned char byte, size_t nbytes, hipStream_t s) {
+  if (!nbytes) return;
+  hipLaunchKernelGGL(k_fill, dim3(grid1d((long)((nbytes + 15) / 16))), dim3(256), 0, s, (unsigned char*)p, nbytes,
+                     (unsigned)byte);
+}
+void copy_async(float* dst, const float* src, long n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy32, dim3(grid1d((n + 3) / 4)), dim3(256), 0, s, dst, src, n);
 }
 
 // ---- dispatch helpers
@@ -841,13 +860,13 @@ int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_s
   return GGNN_OK;
 }
 
-int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate, float beta1, float beta2,
-                   float epsilon, float clip_norm, int64_t step, float grad_scale, float* scratch,
-                   ggnn_stream_t stream) {
+static int adam_impl(const ggnn_adam_tensor* tensors, int count, float learning_rate, float beta1, float beta2,
+                     float epsilon, float clip_norm, int64_t step, const int64_t* step_dev, float grad_scale,
+                     float* scratch, ggnn_stream_t stream) {
   if (!tensors || !scratch) return fail(GGNN_EINVAL, "adam_step: NULL pointer");
   if (count < 1 || count > GGNN_OPT_MAXT)
     return fail(GGNN_EINVAL, "adam_step: count must be in 1.." + std::to_string(GGNN_OPT_MAXT));
-  if (step < 1) return fail(GGNN_EINVAL, "adam_step: step counts from 1");
+  if (!step_dev && step < 1) return fail(GGNN_EINVAL, "adam_step: step counts from 1");
   if (!(clip_norm > 0.f)) return fail(GGNN_EINVAL, "adam_step: clip_norm must be > 0");
   OptArgs a;
   memset(&a, 0, sizeof(a));
@@ -862,8 +881,13 @@ int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_ra
   }
   a.begin[count] = off;
   // TF1 Adam folds both bias corrections into the step size
-  const double b1t = std::pow((double)beta1, (double)step), b2t = std::pow((double)beta2, (double)step);
-  a.lr_t = (float)(learning_rate * std::sqrt(1.0 - b2t) / (1.0 - b1t));
+  if (step_dev) {
+    a.step = step_dev;
+    a.lr = learning_rate;
+  } else {
+    const double b1t = std::pow((double)beta1, (double)step), b2t = std::pow((double)beta2, (double)step);
+    a.lr_t = (float)(learning_rate * std::sqrt(1.0 - b2t) / (1.0 - b1t));
+  }
   a.gscale = grad_scale;
   a.clip = clip_norm;
   a.b1 = beta1;
@@ -879,6 +903,19 @@ int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_ra
   hipLaunchKernelGGL(k_opt_adam, grid, dim3(256), 0, s, a, (const float*)scratch);
   LAUNCHCHK();
   return GGNN_OK;
+}
+int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate, float beta1, float beta2,
+                   float epsilon, float clip_norm, int64_t step, float grad_scale, float* scratch,
+                   ggnn_stream_t stream) {
+  return adam_impl(tensors, count, learning_rate, beta1, beta2, epsilon, clip_norm, step, nullptr, grad_scale, scratch,
+                   stream);
+}
+int ggnn_adam_step_dev(const ggnn_adam_tensor* tensors, int count, float learning_rate, float beta1, float beta2,
+                       float epsilon, float clip_norm, const int64_t* step, float grad_scale, float* scratch,
+                       ggnn_stream_t stream) {
+  if (!step) return fail(GGNN_EINVAL, "adam_step_dev: NULL step");
+  return adam_impl(tensors, count, learning_rate, beta1, beta2, epsilon, clip_norm, 0, step, grad_scale, scratch,
+                   stream);
 }
 
 int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges, const int32_t* graph_offsets,
@@ -901,8 +938,8 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
   const AdjL L = adj_layout(c);
   const size_t tiles = (size_t)c.b * c.C;
   Prof p(K_ADJ, s);
-  HIPCHK(hipMemsetAsync(P<u16>(adj, L.Ab), 0, tiles * c.V * c.V * 2, s));
-  HIPCHK(hipMemsetAsync(P<u16>(adj, L.AbT), 0, tiles * c.V * c.V * 2, s));
+  fill_async(P<u16>(adj, L.Ab), 0, tiles * c.V * c.V * 2, s);
+  fill_async(P<u16>(adj, L.AbT), 0, tiles * c.V * c.V * 2, s);
   const int grid = grid1d(std::max<int64_t>(num_edges, 1));
 #define ADJ_EDGES(VV, F)                                                                                         \
   do {                                                                                                           \
@@ -1088,7 +1125,9 @@ static int emb_args(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg
   a->ncols = ncols;
   a->H = d->h;
   a->rows = (long)d->b * d->v;
-  a->dr = make_drop(keep, seed);
+  if ((d->flags & GGNN_SEED_DEVICE) && !seed && keep < 1.0f)
+    return fail(GGNN_EINVAL, std::string(what) + ": GGNN_SEED_DEVICE needs a device seed address");
+  a->dr = make_drop(keep, seed, (d->flags & GGNN_SEED_DEVICE) != 0);
   return GGNN_OK;
 }
 
@@ -1180,19 +1219,23 @@ int ggnn_heads_workspace_bytes(const ggnn_dims* d, const ggnn_output_head* heads
   return GGNN_OK;
 }
 
-int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
-                       float keep, uint64_t seed, float target_num, float* loss, void* ws, ggnn_stream_t stream) {
+// target_num: a host value, or (tn_dev) read from device memory by the kernels
+static int heads_forward_impl(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                              const float* h0, float keep, uint64_t seed, float target_num, const float* tn_dev,
+                              float* loss, void* ws, ggnn_stream_t stream) {
   HeadL L;
   if (int e = head_layout(d, heads, nheads, &L, "heads_forward")) return e;
   if (int e = check_keep(keep, "heads_forward")) return e;
   if (!hT || !h0 || !ws) return fail(GGNN_EINVAL, "heads_forward: NULL pointer");
-  if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_forward: target_num must be > 0");
+  if (!tn_dev && !(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_forward: target_num must be > 0");
+  if ((d->flags & GGNN_SEED_DEVICE) && !seed && keep < 1.0f)
+    return fail(GGNN_EINVAL, "heads_forward: GGNN_SEED_DEVICE needs a device seed address");
   for (int i = 0; i < nheads; ++i)
     if (!heads[i].probs) return fail(GGNN_EINVAL, "heads_forward: NULL probs");
   hipStream_t s = (hipStream_t)stream;
   const int H = d->h, K = 2 * H, Ot = L.Ot;
   const long rows = (long)d->b * d->v;
-  const Drop dr = make_drop(keep, seed);
+  const Drop dr = make_drop(keep, seed, (d->flags & GGNN_SEED_DEVICE) != 0);
   Prof p(K_HEADS, s);
   float* W = P<float>(ws, L.W);
   float* Z = P<float>(ws, L.Z);
@@ -1218,7 +1261,7 @@ int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nh
     float* lp = P<float>(ws, L.lp) + (long)i * HEAD_LP;
 #define HSM(NI_)                                                                                                  \
   hipLaunchKernelGGL(k_head_softmax<NI_>, dim3(nb), dim3(256), 0, s, Z + L.off[i], Ot, hd.probs, y, rows, o, \
-                     1.0f / target_num, lp)
+                     tn_dev ? 1.0f : 1.0f / target_num, tn_dev, lp)
     if (o <= 64) HSM(1);
     else if (o <= 128) HSM(2);
     else if (o <= 256) HSM(4);
@@ -1229,14 +1272,24 @@ int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nh
   LAUNCHCHK();
   return GGNN_OK;
 }
+int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
+                       float keep, uint64_t seed, float target_num, float* loss, void* ws, ggnn_stream_t stream) {
+  return heads_forward_impl(d, heads, nheads, hT, h0, keep, seed, target_num, nullptr, loss, ws, stream);
+}
+int ggnn_heads_forward_dev(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                           const float* h0, float keep, uint64_t seed, const float* target_num, float* loss, void* ws,
+                           ggnn_stream_t stream) {
+  if (!target_num) return fail(GGNN_EINVAL, "heads_forward_dev: NULL target_num");
+  return heads_forward_impl(d, heads, nheads, hT, h0, keep, seed, 0.f, target_num, loss, ws, stream);
+}
 
-int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
-                        float target_num, const float* d_loss, void* ws, float* dhT, float* dh0,
-                        ggnn_stream_t stream) {
+static int heads_backward_impl(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                               const float* h0, float target_num, const float* tn_dev, const float* d_loss, void* ws,
+                               float* dhT, float* dh0, ggnn_stream_t stream) {
   HeadL L;
   if (int e = head_layout(d, heads, nheads, &L, "heads_backward")) return e;
   if (!hT || !h0 || !ws || !dhT || !dh0) return fail(GGNN_EINVAL, "heads_backward: NULL pointer");
-  if (!(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_backward: target_num must be > 0");
+  if (!tn_dev && !(target_num > 0.f)) return fail(GGNN_EINVAL, "heads_backward: target_num must be > 0");
   hipStream_t s = (hipStream_t)stream;
   const int H = d->h, K = 2 * H, Ot = L.Ot;
   const long rows = (long)d->b * d->v;
@@ -1256,8 +1309,8 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
     const int o = hd.o, op = (o + 3) & ~3;
     const dim3 g((unsigned)std::min<long>(256, (rows + 15) / 16));  // (bias atomics: one per column per block)
 #define HDZ(NI_)                                                                                                  \
-  hipLaunchKernelGGL(k_head_dz<NI_>, g, dim3(256), 0, s, hd.probs, hd.labels, rows, o, op, 1.0f / target_num, d_loss, \
-                     dZ + L.off[i], Ot, hd.d_bias)
+  hipLaunchKernelGGL(k_head_dz<NI_>, g, dim3(256), 0, s, hd.probs, hd.labels, rows, o, op,                       \
+                     tn_dev ? 1.0f : 1.0f / target_num, tn_dev, d_loss, dZ + L.off[i], Ot, hd.d_bias)
     if (op <= 64) HDZ(1);
     else if (op <= 128) HDZ(2);
     else if (op <= 256) HDZ(4);
@@ -1266,9 +1319,8 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
   }
   // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
   // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
-  int ex = 0;
-  frexpf(target_num, &ex);
-  const float S = ldexpf(1.0f, std::max(-100, std::min(100, ex - 1)));
+  // (tn_dev: the GEMMs resolve S from the device value, GemmArgs::snum)
+  const float S = tn_dev ? 2.0f : tnum_scale(target_num);
   const float* W = P<const float>(ws, L.W);
   // (hidden a multiple of 64: each product in one launch with the output /
   // operand split at H; otherwise one launch per half)
@@ -1277,7 +1329,7 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
   for (int half = 0; half < (one ? 1 : 2); ++half) {
     // [dhT | dh0] = dZ W^T  (B(k=j, n=c) = W[c][j]; K = Ot: padding columns are zeros)
     GemmArgs q = gg_args();
-    q.A = dZ; q.sAm = Ot; q.sAk = 1; q.scA = S; q.alpha = 1.0f / S;
+    q.A = dZ; q.sAm = Ot; q.sAk = 1; q.scA = S; q.alpha = 1.0f / S; q.snum = tn_dev; q.sdev = 1;
     q.B = W + (long)half * H * Ot; q.sBk = 1; q.sBn = Ot;
     q.D = half ? dh0 : dhT; q.sDm = H; q.sDn = 1;
     q.M = (int)rows; q.N = one ? 2 * H : H; q.K = Ot;
@@ -1286,7 +1338,7 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
     // dW[rows of the half] += (mask / keep) * ([hT | h0]^T dZ): split-K over node rows, atomics
     GemmArgs w = gg_args();
     w.A = half ? h0 : hT; w.sAp = KC * H; w.sAm = 1; w.sAk = H;
-    w.B = dZ; w.sBp = KC * Ot; w.sBk = Ot; w.sBn = 1; w.scB = S; w.alpha = 1.0f / S;
+    w.B = dZ; w.sBp = KC * Ot; w.sBk = Ot; w.sBn = 1; w.scB = S; w.alpha = 1.0f / S; w.snum = tn_dev; w.sdev = 2;
     w.D = dW + (long)half * H * Ot; w.sDm = Ot; w.sDn = 1; w.mode = GG_ATOMIC;
     w.E = P<const float>(ws, L.Sx) + (long)half * H * Ot;
     w.Z = (int)((rows + KC - 1) / KC); w.M = one ? 2 * H : H; w.N = Ot; w.K = (int)KC; w.Ktot = rows; w.sKp = KC;
@@ -1298,6 +1350,17 @@ int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int n
                        heads[i].o, heads[i].d_weight);
   LAUNCHCHK();
   return GGNN_OK;
+}
+int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT, const float* h0,
+                        float target_num, const float* d_loss, void* ws, float* dhT, float* dh0,
+                        ggnn_stream_t stream) {
+  return heads_backward_impl(d, heads, nheads, hT, h0, target_num, nullptr, d_loss, ws, dhT, dh0, stream);
+}
+int ggnn_heads_backward_dev(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                            const float* h0, const float* target_num, const float* d_loss, void* ws, float* dhT,
+                            float* dh0, ggnn_stream_t stream) {
+  if (!target_num) return fail(GGNN_EINVAL, "heads_backward_dev: NULL target_num");
+  return heads_backward_impl(d, heads, nheads, hT, h0, 0.f, target_num, d_loss, ws, dhT, dh0, stream);
 }
 
 }  // extern "C"

@@ -37,6 +37,7 @@ typedef uint4 frag;
 typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 
 #define DEV __device__ __forceinline__
+#define HDI __host__ __device__ inline
 #ifdef GGNN_TS
 __device__ unsigned long long g_ts[4][2048 * 8];
 #define TSMARK(k, i) do { if (threadIdx.x == 0) g_ts[k][blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -280,7 +281,13 @@ struct Drop {
   uint32_t k0, k1;  // key = seed
   uint32_t thr;     // 0 = dropout off
   float scale;      // 1 / keep
+  // GGNN_SEED_DEVICE: the key is read from device memory at run time
+  // (kp[0] = low, kp[1] = high word of the uint64 seed), so a captured
+  // hipGraph replays with each step's fresh seed
+  const uint32_t* kp;
 };
+DEV uint32_t dkey0(const Drop& d) { return d.kp ? d.kp[0] : d.k0; }
+DEV uint32_t dkey1(const Drop& d) { return d.kp ? d.kp[1] : d.k1; }
 DEV uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -294,10 +301,10 @@ DEV uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 }
 DEV uint32_t u4_get(const uint4& w, int j) { return j == 0 ? w.x : j == 1 ? w.y : j == 2 ? w.z : w.w; }
 DEV uint4 state_words(const Drop& d, int g, int i, int k, int t) {
-  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)k, (uint32_t)g, 0x80000000u | (uint32_t)t), d.k0, d.k1);
+  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)k, (uint32_t)g, 0x80000000u | (uint32_t)t), dkey0(d), dkey1(d));
 }
 DEV uint4 edge_words(const Drop& d, int c, int i, int j, int t) {
-  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)c, (uint32_t)t), d.k0, d.k1);
+  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)c, (uint32_t)t), dkey0(d), dkey1(d));
 }
 DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x * d.scale : 0.0f; }
 

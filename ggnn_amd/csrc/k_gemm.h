@@ -75,7 +75,35 @@ struct GemmArgs {
   // dW (Philox counter (m>>2, n, zp, t), word m&3: one block per row quad)
   Drop dr;
   int drop_t;
+  // if set: the scales come from a device float t (the heads' target_num,
+  // ggnn_heads_backward_dev): S = tnum_scale(*snum) replaces scA (sdev bit 0)
+  // and / or scB (bit 1), and alpha = 1 / S
+  const float* snum;
+  int sdev;
 };
+
+// exact power of two S <= t carrying the heads' dZ ~ 1/t into the f16 normal
+// range (frexp exponent e: S = 2^(e-1), clamped to 2^+-100); host and device
+HDI float tnum_scale(float t) {
+  int ex = 0;
+  frexpf(t, &ex);
+  const int e = ex - 1 < -100 ? -100 : ex - 1 > 100 ? 100 : ex - 1;
+  return ldexpf(1.0f, e);
+}
+// the operand scales and alpha of one launch (device-resolved under snum)
+struct GemmScales {
+  float sa, sb, alpha;
+};
+DEV GemmScales gemm_scales(const GemmArgs& a) {
+  GemmScales g{a.scA, a.scB, a.alpha};
+  if (a.snum) {
+    const float S = tnum_scale(*a.snum);
+    if (a.sdev & 1) g.sa = S;
+    if (a.sdev & 2) g.sb = S;
+    g.alpha = 1.0f / S;
+  }
+  return g;
+}
 
 namespace gg {
 constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
@@ -204,6 +232,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
   const int wm = w & 1, wn = w >> 1;
   const int n0 = blockIdx.x * BNt, m0 = blockIdx.y * BMt;
   const int kc = (a.K + BK - 1) / BK;
+  const GemmScales gs = gemm_scales(a);
 
   for (int z = blockIdx.z; z < a.Z; z += gridDim.z) {
     if (a.zmask && !a.zmask[z]) continue;
@@ -234,13 +263,13 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
           gg_load<AKC, true, F16>(ra + 8 * i, Ab, abase, a.sAm, a.sAk, am0 + 64 * i, aM, kk0, a.K, kg0, a.Ktot, 1.0f,
                                   tid);
         else
-          gg_load<AKC, false, F16>(ra + 8 * i, Ab, abase, a.sAm, a.sAk, am0 + 64 * i, aM, kk0, a.K, kg0, a.Ktot, a.scA,
+          gg_load<AKC, false, F16>(ra + 8 * i, Ab, abase, a.sAm, a.sAk, am0 + 64 * i, aM, kk0, a.K, kg0, a.Ktot, gs.sa,
                                    tid);
       }
 #pragma unroll
       for (int j = 0; j < WN; ++j)
         gg_load<BKC, false, F16>(rb + 8 * j, a.B, p * a.sBp + q * a.sBq, a.sBn, a.sBk, n0 + 64 * j, a.N, kk0, a.K, kg0,
-                                 a.Ktot, a.scB, tid);
+                                 a.Ktot, gs.sb, tid);
     };
     // ---- registers -> LDS limb images ([row][k], k contiguous)
     auto store = [&](int buf) {
@@ -314,7 +343,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
             const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
             if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
             if (m >= a.M) continue;
-            float x = a.alpha * acc[i][j][r] + bn;
+            float x = gs.alpha * acc[i][j][r] + bn;
             if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
             else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
             if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);

@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   static_assert(!A16 || AKC, "16-bit A operands are k-contiguous");
   static_assert(BMT == 128 || (BMT == 32 && AKC), "32-row tiles: k-contiguous A only");
+  const GemmScales gs = gemm_scales(a);
   constexpr int BM = BMT;
   constexpr int WMW = BMT == 128 ? 2 : 1, WNW = 4 / WMW;  // wave grid
   constexpr int AM = BMT / (32 * WMW), AN = BN / (32 * WNW);  // accumulators per wave
@@ -218,7 +219,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   auto compute = [&](const char* buf) {
     const char* ia = buf;
     const char* ib = buf + AB;
-    const float sa = a.scA, sb = a.scB;
+    const float sa = gs.sa, sb = gs.sb;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int k0 = 16 * s + 8 * hh;
@@ -298,7 +299,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
           const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
           if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
           if (m >= a.M) continue;
-          float x = a.alpha * acc[i][j][r] + bn;
+          float x = gs.alpha * acc[i][j][r] + bn;
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
           if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);

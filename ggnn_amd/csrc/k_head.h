@@ -31,7 +31,7 @@ struct EmbArgs {
 };
 // embedding dropout mask of element (row r, column k): counter (r>>2, k, 0, 0xC0000000), word r&3
 DEV uint4 emb_words(const Drop& d, long r, int k) {
-  return philox4x32_10(make_uint4((uint32_t)(r >> 2), (uint32_t)k, 0u, 0xC0000000u), d.k0, d.k1);
+  return philox4x32_10(make_uint4((uint32_t)(r >> 2), (uint32_t)k, 0u, 0xC0000000u), dkey0(d), dkey1(d));
 }
 DEV int emb_find(const EmbArgs& a, int k) {
   int s = -1;
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
 // ---------------------------------------------------------------------------
 // out-layer weight dropout mask of W[i][j] of head hd: counter (i>>2, j, hd, 0xA0000000), word i&3
 DEV uint4 head_words(const Drop& d, int hd, int i, int j) {
-  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)hd, 0xA0000000u), d.k0, d.k1);
+  return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)hd, 0xA0000000u), dkey0(d), dkey1(d));
 }
 // head hd's columns [off, off + op) of the concatenated W * mask / keep and
 // mask / keep ([K][Ot], K = 2H; op = o rounded up to 4, padding zeros) and of
@@ -174,8 +174,9 @@ __global__ void __launch_bounds__(256) k_head_loss(const float* __restrict__ lp,
 template <int NI>
 __global__ void __launch_bounds__(256) k_head_softmax(const float* __restrict__ zin, int zs, float* __restrict__ pout,
                                                       const float* __restrict__ y, long rows, int o, float inv_num,
-                                                      float* __restrict__ lpart) {
+                                                      const float* __restrict__ num_dev, float* __restrict__ lpart) {
   const int lane = threadIdx.x & 63;
+  if (num_dev) inv_num = 1.0f / *num_dev;  // (ggnn_heads_forward_dev: target_num in device memory)
   const long stride = (long)gridDim.x * 4;
   float term = 0.f;
   // two rows per wave and iteration: both rows' loads in flight together
@@ -234,10 +235,12 @@ __global__ void __launch_bounds__(256) k_head_softmax(const float* __restrict__ 
 // with zeros; the row's p and y held in registers)
 template <int NI>
 __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, const float* __restrict__ y, long rows,
-                                                 int o, int op, float inv_num, const float* __restrict__ dloss,
-                                                 float* __restrict__ dZ, int ldz, float* __restrict__ db) {
+                                                 int o, int op, float inv_num, const float* __restrict__ num_dev,
+                                                 const float* __restrict__ dloss, float* __restrict__ dZ, int ldz,
+                                                 float* __restrict__ db) {
   __shared__ float cs[4][NI * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (num_dev) inv_num = 1.0f / *num_dev;
   const float g = (dloss ? *dloss : 1.0f) * inv_num;
   float part[NI];
 #pragma unroll

@@ -23,6 +23,10 @@ struct OptArgs {
   long begin[GGNN_OPT_MAXT + 1];  // prefix offsets over the concatenated elements
   int count;
   float gscale, clip, lr_t, b1, b2, eps;
+  // ggnn_adam_step_dev: the step count is read from device memory and lr_t
+  // derived from it in-kernel (lr = the undecayed rate)
+  const int64_t* step;
+  double lr;
 };
 
 // per-tensor sum of (gscale * g)^2 into sq[tensor]; blockIdx.y = tensor,
@@ -56,7 +60,15 @@ __global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict
 
 __global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __restrict__ sq) {
   const OptTensor& T = a.t[blockIdx.y];
-  __shared__ float tot;
+  __shared__ float tot, lr_t;
+  if (threadIdx.x == 64) {
+    if (a.step) {  // TF1 Adam folds both bias corrections into the step size
+      const double t = (double)*a.step;
+      lr_t = (float)(a.lr * sqrt(1.0 - pow((double)a.b2, t)) / (1.0 - pow((double)a.b1, t)));
+    } else {
+      lr_t = a.lr_t;
+    }
+  }
   if (threadIdx.x < 64) {  // this tensor's squared norm from the sqnorm launch's partials
     float x = 0.f;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += 64) x += sq[blockIdx.y * gridDim.x + i];
@@ -70,7 +82,7 @@ __global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __rest
     const float g = gg * scale;
     m = a.b1 * m + (1.0f - a.b1) * g;
     v = a.b2 * v + (1.0f - a.b2) * g * g;
-    p -= a.lr_t * m / (sqrtf(v) + a.eps);
+    p -= lr_t * m / (sqrtf(v) + a.eps);
   };
   const long st = (long)gridDim.x * blockDim.x;
   long e = (long)blockIdx.x * blockDim.x + threadIdx.x;

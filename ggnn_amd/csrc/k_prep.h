@@ -476,6 +476,35 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
 // ---- zero the backward's gradient accumulators in one launch (they are
 // accumulated by atomics / per-step adds), instead of one hipMemsetAsync per
 // buffer (each a separate ~5 us fill dispatch).  blockIdx.y = buffer.
+// byte fill / fp32 copy as kernels rather than hipMemsetAsync / hipMemcpyAsync:
+// a step captured into a hipGraph then holds kernel nodes only (memset nodes
+// captured from a stream were seen to race with their neighbouring kernels on
+// replay).  k_fill: n bytes of `byte` at p (any alignment; 16-byte pieces over
+// the aligned middle, single bytes at the ends)
+__global__ void __launch_bounds__(256) k_fill(unsigned char* __restrict__ p, size_t n, unsigned byte) {
+  const size_t mis = (size_t)((16 - ((uintptr_t)p & 15)) & 15);
+  const size_t head = mis < n ? mis : n;
+  const size_t body = (n - head) & ~(size_t)15;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, st = (size_t)gridDim.x * blockDim.x;
+  const unsigned w = byte * 0x01010101u;
+  const uint4 v = make_uint4(w, w, w, w);
+  uint4* q = (uint4*)(p + head);
+  for (size_t i = tid; i < body / 16; i += st) q[i] = v;
+  if (tid < head) p[tid] = (unsigned char)byte;
+  const size_t t0 = head + body;
+  if (tid < n - t0) p[t0 + tid] = (unsigned char)byte;
+}
+// dst[0, n) = src[0, n), fp32 (16-byte pieces when both are 16-byte aligned)
+__global__ void __launch_bounds__(256) k_copy32(float* __restrict__ dst, const float* __restrict__ src, long n) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x, st = (long)gridDim.x * blockDim.x;
+  long i = tid;
+  if (((((uintptr_t)dst) | ((uintptr_t)src)) & 15) == 0) {
+    for (; 4 * i + 3 < n; i += st) *(float4*)(dst + 4 * i) = *(const float4*)(src + 4 * i);
+    i = (n & ~3L) + tid;
+  }
+  for (; i < n; i += st) dst[i] = src[i];
+}
+
 #define ZERO_MAXJ 16
 struct ZeroJobs {
   float* p[ZERO_MAXJ];

@@ -52,6 +52,7 @@ class WeightPack:
     T: int = 1
     edge_keep: float = 1.0
     seed: int = 0
+    seed_device: bool = False   # seed is the address of a device uint64 (GGNN_SEED_DEVICE)
 
 
 class PropagationEngine:
@@ -104,9 +105,10 @@ class PropagationEngine:
 
     # ------------------------------------------------------------------ utils
     def dims(self, b: int, v: int, T: int, edge_keep: float = 1.0, state_keep: float = 1.0,
-             seed: int = 0) -> _lib.GGNNDims:
+             seed: int = 0, seed_device: bool = False) -> _lib.GGNNDims:
         d = _lib.dims(b, v, self.h, self.C, T, self.use_edge_bias, self.precision, edge_keep, state_keep, seed,
-                      self.skip_empty_channels, self.force_generic, self.unfused_forward, self._sparse)
+                      self.skip_empty_channels, self.force_generic, self.unfused_forward, self._sparse,
+                      seed_device)
         _lib.check_dims(d)
         return d
 
@@ -122,12 +124,15 @@ class PropagationEngine:
         return ws
 
     # ---------------------------------------------------------------- weights
-    def pack_weights(self, weights: dict, T: int = 1, edge_keep: float = 1.0, seed: int = 0) -> WeightPack:
+    def pack_weights(self, weights: dict, T: int = 1, edge_keep: float = 1.0, seed: int = 0,
+                     seed_device: bool = False) -> WeightPack:
         """weights: dict of fp32 device tensors with the reference's shapes:
         edge_weights [C,h,h], edge_biases [C,1,h] (or [C,h]), gates_kernel [2h,2h],
         gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h].
         edge_keep < 1: edge-weight dropout (chem_tensorflow_dense.py:397-403),
-        one fresh mask per timestep of a T-step pass, keyed by seed."""
+        one fresh mask per timestep of a T-step pass, keyed by seed.
+        seed_device: seed is the address of a device uint64 holding the seed
+        (read when the kernels run: hipGraph capture, ggnn_amd/graphs.py)."""
         h, C = self.h, self.C
         _require(weights["edge_weights"], (C, h, h), "edge_weights")
         eb = weights.get("edge_biases") if self.use_edge_bias else None
@@ -140,14 +145,14 @@ class PropagationEngine:
         _require(weights["candidate_kernel"], (2 * h, h), "candidate_kernel")
         _require(weights["candidate_bias"], (h,), "candidate_bias")
         T = int(T) if edge_keep < 1.0 else 1
-        d = self.dims(1, 1, T, edge_keep=edge_keep, seed=seed)
+        d = self.dims(1, 1, T, edge_keep=edge_keep, seed=seed, seed_device=seed_device)
         buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)
         _lib.check(self._lib.ggnn_pack_weights(
             ctypes.byref(d), _ptr(buf), _ptr(weights["edge_weights"]), _ptr(eb),
             _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
             _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream()),
             "ggnn_pack_weights")
-        return WeightPack(buf, h, C, self.use_edge_bias, T, float(edge_keep), int(seed))
+        return WeightPack(buf, h, C, self.use_edge_bias, T, float(edge_keep), int(seed), bool(seed_device))
 
     # -------------------------------------------------------------- adjacency
     def set_adjacency(self, adjacency: torch.Tensor) -> None:
@@ -240,7 +245,7 @@ class PropagationEngine:
         if pack.edge_keep < 1.0 and pack.T != T:
             raise ValueError("the pack holds edge-dropout masks for T=%d, forward asked for T=%d" % (pack.T, T))
         ws = self.workspace(b, v, T, training, pack.edge_keep < 1.0)
-        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed)
+        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed, pack.seed_device)
         if out is None:
             out = torch.empty((b, v, self.h), dtype=torch.float32, device=self.device)
         _require(out, (b, v, self.h), "out")
@@ -271,7 +276,7 @@ class PropagationEngine:
         _require(dhT, (b, v, self.h), "dL/dh_T")
         if grads is None:
             grads = self.alloc_grads(b, v)
-        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed)
+        d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed, pack.seed_device)
         _lib.check(self._lib.ggnn_backward(
             ctypes.byref(d), _ptr(pack.buf), _ptr(self._adj), _ptr(ws), _ptr(dhT), _ptr(grads["h0"]),
             _ptr(grads["edge_weights"]), _ptr(grads.get("edge_biases")), _ptr(grads["gates_kernel"]),

@@ -85,16 +85,19 @@ class EmbeddingFrontEnd:
                                   t.shape[1], int(col))
         return arr
 
-    def forward(self, segments, wi: torch.Tensor, keep: float = 1.0, seed: int = 0) -> torch.Tensor:
+    def forward(self, segments, wi: torch.Tensor, keep: float = 1.0, seed: int = 0, seed_device: bool = False,
+                out=None) -> torch.Tensor:
+        """seed_device: seed is the address of a device uint64 (GGNN_SEED_DEVICE)."""
         b, v, ncols = wi.shape
-        h0 = torch.empty(b, v, self.hidden, dtype=torch.float32, device=wi.device)
-        d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32")
+        h0 = out if out is not None else torch.empty(b, v, self.hidden, dtype=torch.float32, device=wi.device)
+        d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32", seed_device=seed_device)
         _lib.check(self._lib.ggnn_embed_forward(ctypes.byref(d), self._segs(segments), len(segments), _ptr(wi), ncols,
                                                 float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(h0), _stream()),
                    "ggnn_embed_forward")
         return h0
 
-    def backward(self, segments, wi, dh0, keep=1.0, seed=0, dh0_add=None, dtables=None, sq_out=None):
+    def backward(self, segments, wi, dh0, keep=1.0, seed=0, dh0_add=None, dtables=None, sq_out=None,
+                 seed_device=False):
         """Returns (per-segment dense table gradients, lookup sqnorm device
         vector [nseg]).  dtables: optional per-segment gradient buffers;
         segments that share a table may share one buffer (the kernel adds both
@@ -104,7 +107,7 @@ class EmbeddingFrontEnd:
         b, v, ncols = wi.shape
         dts = dtables if dtables is not None else [torch.empty_like(t) for t, _ in segments]
         sq = sq_out if sq_out is not None else torch.empty(len(segments), dtype=torch.float32, device=wi.device)
-        d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32")
+        d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32", seed_device=seed_device)
         _lib.check(self._lib.ggnn_embed_backward(ctypes.byref(d), self._segs(segments, dts), len(segments), _ptr(wi),
                                                  ncols, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                  _ptr(dh0.contiguous()), _ptr(None if dh0_add is None else
@@ -132,14 +135,18 @@ class OutputHeads:
                                 None if dbs is None else dbs[i].data_ptr())
         return arr
 
-    def forward(self, hT, h0, heads, labels=None, keep=1.0, seed=0, target_num=1.0, loss_out=None, probs_out=None):
+    def forward(self, hT, h0, heads, labels=None, keep=1.0, seed=0, target_num=1.0, loss_out=None, probs_out=None,
+                seed_device=False):
         """Returns (probs list [b, v, o], loss tensor [nheads] or None).
-        loss_out / probs_out: optional output buffers (loss [nheads] fp32)."""
+        loss_out / probs_out: optional output buffers (loss [nheads] fp32).
+        target_num: a number, or a device fp32 tensor of one element
+        (ggnn_heads_forward_dev); seed_device: seed is the address of a
+        device uint64 (GGNN_SEED_DEVICE)."""
         b, v, h = hT.shape
         dev = hT.device
         probs = probs_out if probs_out is not None else [torch.empty(b, v, W.shape[1], dtype=torch.float32, device=dev)
                                                           for W, _ in heads]
-        d = _lib.dims(b, v, h, 1, 1, True, "fp32")
+        d = _lib.dims(b, v, h, 1, 1, True, "fp32", seed_device=seed_device)
         tab = self._table(heads, labels, probs)
         n = ctypes.c_size_t(0)
         _lib.check(self._lib.ggnn_heads_workspace_bytes(ctypes.byref(d), tab, len(heads), ctypes.byref(n)),
@@ -149,10 +156,17 @@ class OutputHeads:
         loss = None
         if labels is not None:
             loss = loss_out if loss_out is not None else torch.empty(len(heads), dtype=torch.float32, device=dev)
-        _lib.check(self._lib.ggnn_heads_forward(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
-                                                _ptr(h0.contiguous()), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                                                float(target_num), _ptr(loss), _ptr(self._ws), _stream()),
-                   "ggnn_heads_forward")
+        if isinstance(target_num, torch.Tensor):
+            _lib.check(self._lib.ggnn_heads_forward_dev(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
+                                                        _ptr(h0.contiguous()), float(keep),
+                                                        int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(target_num), _ptr(loss),
+                                                        _ptr(self._ws), _stream()),
+                       "ggnn_heads_forward_dev")
+        else:
+            _lib.check(self._lib.ggnn_heads_forward(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
+                                                    _ptr(h0.contiguous()), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                    float(target_num), _ptr(loss), _ptr(self._ws), _stream()),
+                       "ggnn_heads_forward")
         self._saved = (b, v, h)
         return probs, loss
 
@@ -169,11 +183,17 @@ class OutputHeads:
         dhT = dhT if dhT is not None else torch.empty_like(hT)
         dh0 = dh0 if dh0 is not None else torch.empty_like(h0)
         d = _lib.dims(b, v, h, 1, 1, True, "fp32")
-        _lib.check(self._lib.ggnn_heads_backward(ctypes.byref(d), self._table(heads, labels, probs, dws, dbs),
-                                                 len(heads), _ptr(hT.contiguous()), _ptr(h0.contiguous()),
-                                                 float(target_num), _ptr(d_loss), _ptr(self._ws), _ptr(dhT), _ptr(dh0),
-                                                 _stream()),
-                   "ggnn_heads_backward")
+        tab = self._table(heads, labels, probs, dws, dbs)
+        if isinstance(target_num, torch.Tensor):     # device target_num (ggnn_heads_backward_dev)
+            _lib.check(self._lib.ggnn_heads_backward_dev(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
+                                                         _ptr(h0.contiguous()), _ptr(target_num), _ptr(d_loss),
+                                                         _ptr(self._ws), _ptr(dhT), _ptr(dh0), _stream()),
+                       "ggnn_heads_backward_dev")
+        else:
+            _lib.check(self._lib.ggnn_heads_backward(ctypes.byref(d), tab, len(heads), _ptr(hT.contiguous()),
+                                                     _ptr(h0.contiguous()), float(target_num), _ptr(d_loss),
+                                                     _ptr(self._ws), _ptr(dhT), _ptr(dh0), _stream()),
+                       "ggnn_heads_backward")
         return dws, dbs, dhT, dh0
 
 

@@ -41,6 +41,7 @@ from . import evaluation as _eval
 from .batching import BtbBatching, ThreadedIterator
 from .dist import FlatTrainBuffer
 from .engine import PropagationEngine
+from .graphs import CapturedStep, PinnedRing, StepLayout, edge_arrays
 from .heads import SMALL_NUMBER, EmbedFunction, EmbeddingFrontEnd, HeadsFunction, OutputHeads, word_inputs_tensor
 from .optim import ClipAdam
 from .upload import Uploader
@@ -58,6 +59,21 @@ def glorot_init(shape, rng=None):
     rng = np.random if rng is None else rng
     lim = np.sqrt(6.0 / (shape[-2] + shape[-1]))
     return rng.uniform(low=-lim, high=lim, size=shape).astype(np.float32)
+
+
+class _StepFeed:
+    """One step's inputs as the library calls take them: device tensors
+    (word_inputs, labels), the seeds as values or as device addresses
+    (seed_device, GGNN_SEED_DEVICE), target_num as a number or a device
+    scalar, the engine and heads that run the step and how the engine stages
+    the batch's adjacency."""
+
+    def __init__(self, wi, seeds, seed_values, seed_device, labels, target_num, engine, heads, stage, b, v,
+                 target_num_value=None):
+        self.wi, self.seeds, self.seed_values, self.seed_device = wi, seeds, seed_values, seed_device
+        self.labels, self.target_num, self.engine, self.heads, self.stage = labels, target_num, engine, heads, stage
+        self.b, self.v = b, v
+        self.target_num_value = target_num if target_num_value is None else target_num_value
 
 
 class _Propagate(torch.autograd.Function):
@@ -149,6 +165,7 @@ class DenseGGNNChemModel(BtbBatching):
             "graph_state_dropout_keep_prob": 0.9, "task_sample_ratios": {}, "use_edge_bias": True,
             "edge_weight_dropout_keep_prob": 1,
             "compact_adjacency": False,   # not in the reference: edge-list feed (ggnn_set_adjacency_edges)
+            "hip_graphs": True,           # not in the reference: captured steps for edge-list feeds (graphs.py)
         }
 
     @property
@@ -193,6 +210,9 @@ class DenseGGNNChemModel(BtbBatching):
         self._front_end = None
         self._heads = None
         self._flat = None
+        self._graphs = {}           # hipGraph-captured steps by batch shape (graphs.py)
+        self._ring = None
+        self.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
         self.lookup_sqnorm = {}
         self.optimizer = None
 
@@ -419,6 +439,11 @@ class DenseGGNNChemModel(BtbBatching):
         without a batch in the last global step) contributes zeros."""
         if feed_dict is not None and int(feed_dict.get("num_graphs", 1)) == 0:
             return self._empty_train_step(all_reduce, grad_scale)
+        if feed_dict is not None and self._graph_ok(feed_dict):
+            loss = self._graph_step(feed_dict, True, task_id, target_count, all_reduce, grad_scale)
+            if loss is not None:
+                return loss
+        self.graph_stats["eager"] += 1
         if feed_dict is not None:
             self.feed(feed_dict)
         if target_count is None:
@@ -439,7 +464,142 @@ class DenseGGNNChemModel(BtbBatching):
         self._apply_gradients(fl, self.trainable_variables(), grad_scale)
         return fl.loss.sum()
 
-    def _apply_gradients(self, fl, params, grad_scale):
+    # ------------------------------------------- hipGraph capture (graphs.py)
+    def _graph_ok(self, feed) -> bool:
+        """Whether a feed can run as a captured step: a compact (edge-list)
+        batch on the GPU, params['hip_graphs'] on."""
+        return (bool(self.params.get("hip_graphs", True)) and self.device.type == "cuda"
+                and feed.get("adjacency_matrix") is None and feed.get("adjacency_edges") is not None
+                and "word_inputs" in feed and int(feed.get("num_graphs", 0)) > 0
+                and self.args.get("--pr", "btb") == "btb")
+
+    def _graph_step(self, feed, training, task_id=0, target_count=None, all_reduce=None, grad_scale=1.0):
+        """One batch through its shape's captured step: stage the batch's
+        inputs (one H2D copy), then replay the graph -- or, the first time a
+        shape is seen, run the step's body eagerly on the same device inputs
+        and capture it for the next batches of that shape.  Training: the
+        train_step body (+ clip + Adam inside the graph when there is no
+        all-reduce; otherwise the all-reduce and Adam follow eagerly).
+        Evaluation: the build_loss forward.  Returns the loss (device
+        scalar), or None when the batch does not fit a captured step (more
+        edges than the b * v capacity)."""
+        self.feed(feed)
+        self._check_front_end_width()
+        ph = self.placeholders
+        b, v = int(ph["num_graphs"]), int(ph["num_vertices"])
+        o, oe = self.params["output_size"], self.output_size_edges
+        if v > o:
+            raise ValueError("num_vertices %d > output_size %d" % (v, o))
+        tables, cols = self._front_end_segments()
+        wi = np.asarray(ph["word_inputs"]).astype(np.int64)
+        for tb, c in zip(tables, cols):
+            x = wi[..., c]
+            if x.size and (x.min() < 0 or x.max() >= tb.shape[0]):
+                raise IndexError("word_inputs[..., %d] holds index %d outside [0, %d)"
+                                 % (c, int(x.max() if x.max() >= tb.shape[0] else x.min()), tb.shape[0]))
+        edges, offs = edge_arrays(ph["adjacency_edges"], v, self.num_edge_types)
+        if edges.shape[0] > b * v:
+            return None
+        if target_count is None:
+            target_count = ph.get("global_target_count") if training else None
+        count = self._target_count(task_id) if target_count is None else float(target_count)
+        target_num = float(count + SMALL_NUMBER)
+        keeps = (float(ph.get("emb_dropout_keep_prob", 1.0)),) + self._path_keeps() + (self._out_keep(),)
+        adam = training and all_reduce is None
+        key = (bool(training), adam, b, v, wi.shape[-1], keeps, task_id)
+        if training:
+            fl = self.train_buffer()
+            params = self.trainable_variables()
+            if self.optimizer is None:
+                self.make_optimizer()
+        cs = self._graphs.get(key)
+        if cs is None:
+            eng = PropagationEngine(self.params["hidden_size"], self.num_channels, bool(self.params["use_edge_bias"]),
+                                    device=self.device, precision=self.precision)
+            cs = CapturedStep(StepLayout(b, v, wi.shape[-1], o, oe), eng, OutputHeads(self.params["hidden_size"]),
+                              self.device)
+            self._graphs[key] = cs
+        seeds = [self._seed() for _ in range(3)]
+        step = 0
+        if adam:
+            self.optimizer.t += 1
+            step = self.optimizer.t
+        # stage the batch: pinned host buffer -> the step's device inputs
+        L = cs.layout
+        if self._ring is None:
+            self._ring = PinnedRing()
+        i, host = self._ring.acquire(L.nbytes)
+        L.fill(host.numpy(), seeds, step, target_num, wi.astype(np.int32), edges, offs,
+               np.asarray(ph["target_values_head"], np.float32), np.asarray(ph["target_values_edges"], np.float32))
+        stream = torch.cuda.current_stream(self.device)
+        cs.inputs.buf[:L.nbytes].copy_(host, non_blocking=True)
+        self._ring.release(i, stream)
+        inp = cs.inputs
+        sf = _StepFeed(inp.wi, tuple(inp.seed_address(k) for k in range(3)), tuple(seeds), True, [inp.yh, inp.ye],
+                       inp.target_num, cs.engine, cs.heads,
+                       lambda eng: eng.set_adjacency_edges((inp.edges, inp.offs), v, self.num_edge_types), b, v,
+                       target_num_value=target_num)
+
+        def body():
+            if training:
+                probs = self._forward_backward(fl, params, None, task_id, sf)
+                if adam:
+                    self._apply_gradients(fl, params, 1.0, step_dev=inp.step)
+                loss = fl.loss.sum()
+            else:
+                probs, loss = self._forward_eval(sf, task_id)
+            return {"loss": loss, "probs": probs}
+
+        if cs.graph is None:
+            out = body()                     # the real step for this batch
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                cs.out = body()              # recorded, not executed
+            cs.graph = g
+            self.graph_stats["captured"] += 1
+        else:
+            cs.graph.replay()
+            cs.replays += 1
+            out = cs.out
+            self.graph_stats["replayed"] += 1
+        probs = out["probs"]
+        self.ops["computed_values"] = probs[0].reshape(b, v * o)
+        self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
+        self.ops["loss"] = out["loss"]
+        if training and not adam:
+            all_reduce(fl.flat)
+            self._apply_gradients(fl, params, grad_scale)
+        return out["loss"]
+
+    def _forward_eval(self, sf, task_id=0):
+        """build_loss's forward without autograd on a _StepFeed: front-end ->
+        T-step forward -> heads + btb loss.  Returns (probs, loss sum)."""
+        h = self.params["hidden_size"]
+        tables, cols = self._front_end_segments()
+        keep_e = float(self.placeholders.get("emb_dropout_keep_prob", 1.0))
+        if self._front_end is None:
+            self._front_end = EmbeddingFrontEnd(h)
+        h0 = self._front_end.forward(list(zip(tables, cols)), sf.wi, keep_e, sf.seeds[0], seed_device=sf.seed_device)
+        self.last_embed = dict(keep=keep_e, seed=sf.seed_values[0])
+        T = self.params["num_timesteps"]
+        eng = sf.engine
+        sf.stage(eng)
+        edge_keep, state_keep = self._path_keeps()
+        W, gru = self.weights, self.weights["node_gru"]
+        wts = {"edge_weights": W["edge_weights"],
+               "edge_biases": W["edge_biases"] if self.params["use_edge_bias"] else None,
+               "gates_kernel": gru["gates_kernel"], "gates_bias": gru["gates_bias"],
+               "candidate_kernel": gru["candidate_kernel"], "candidate_bias": gru["candidate_bias"]}
+        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device)
+        hT = eng.forward(h0, pack, T, training=False, state_keep=state_keep)
+        self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=sf.seed_values[1])
+        keep_o = self._out_keep()
+        probs, loss = sf.heads.forward(hT, h0, self._heads_list(task_id), sf.labels, keep_o, sf.seeds[2],
+                                       sf.target_num, seed_device=sf.seed_device)
+        self.last_heads = dict(keep=keep_o, seed=sf.seed_values[2], target_num=sf.target_num_value)
+        return probs, loss.sum()
+
+    def _apply_gradients(self, fl, params, grad_scale, step_dev=None):
         if self.optimizer is None:
             self.make_optimizer()
         tables = self._front_end_segments()[0]
@@ -451,67 +611,80 @@ class DenseGGNNChemModel(BtbBatching):
         sq = [self.lookup_sqnorm.get(id(p)) for p in params]
         for p, g in zip(params, fl.grads):
             p.grad = g
-        self.optimizer.step(fl.grads, grad_scale=grad_scale, sqnorms=sq)
+        self.optimizer.step(fl.grads, grad_scale=grad_scale, sqnorms=sq, step_dev=step_dev)
 
-    def _forward_backward(self, fl, params, target_count, task_id):
+    def _eager_step_feed(self, task_id, target_count) -> "_StepFeed":
+        """The staged batch's inputs as device tensors uploaded now, with
+        fresh seed values (drawn in build_loss's order: front-end, path,
+        heads) and the host target_num."""
+        tables, cols = self._front_end_segments()
+        wi = word_inputs_tensor(self.placeholders["word_inputs"], self.device,
+                                {c: tb.shape[0] for tb, c in zip(tables, cols)})
+        seeds = (self._seed(), self._seed(), self._seed())
+        b, v = int(self.placeholders["num_graphs"]), int(self.placeholders["num_vertices"])
+        labels = self._head_labels(b, v)
+        count = self._target_count(task_id) if target_count is None else target_count
+        if self._heads is None:
+            self._heads = OutputHeads(self.params["hidden_size"])
+        return _StepFeed(wi, seeds, seeds, False, labels, float(count + SMALL_NUMBER), self._engine("main"),
+                         self._heads, self._stage_adjacency, b, v)
+
+    def _check_front_end_width(self):
+        width = self.loc_embedding_size * 2 + self.pos_embedding_size + self.word_embedding_size
+        if width > self.params["hidden_size"]:
+            raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
+                             "(SURVEY F7); pass smaller embedding_sizes" % (width, self.params["hidden_size"]))
+
+    def _forward_backward(self, fl, params, target_count, task_id, sf=None):
         """The btb loss and every gradient of one staged batch, written into
         the flat buffer ``fl`` (no autograd: each backward of the library
-        writes its outputs where the optimizer reads them).  The dropout seeds
-        are drawn in build_loss's order (front-end, path, heads)."""
+        writes its outputs where the optimizer reads them).  ``sf``: the
+        step's inputs (_StepFeed; default: uploaded from the placeholders).
+        Returns the heads' probabilities."""
         if "word_inputs" not in self.placeholders:
             raise RuntimeError("feed() a minibatch with word_inputs first")
         if self.args.get("--pr", "btb") != "btb":
             raise NotImplementedError("only --pr btb is supported by the engine")
+        self._check_front_end_width()
+        if sf is None:
+            sf = self._eager_step_feed(task_id, target_count)
         h = self.params["hidden_size"]
         gv = {id(p): g for p, g in zip(params, fl.grads)}
         # front-end (chem_tensorflow_dense.py:264-306)
         tables, cols = self._front_end_segments()
-        width = self.loc_embedding_size * 2 + self.pos_embedding_size + self.word_embedding_size
-        if width > h:
-            raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
-                             "(SURVEY F7); pass smaller embedding_sizes" % (width, h))
-        wi = word_inputs_tensor(self.placeholders["word_inputs"], self.device,
-                                {c: tb.shape[0] for tb, c in zip(tables, cols)})
         keep_e = float(self.placeholders.get("emb_dropout_keep_prob", 1.0))
-        seed_e = self._seed()
         if self._front_end is None:
             self._front_end = EmbeddingFrontEnd(h)
         segs = list(zip(tables, cols))
-        h0 = self._front_end.forward(segs, wi, keep_e, seed_e)
-        self.last_embed = dict(keep=keep_e, seed=seed_e)
+        h0 = self._front_end.forward(segs, sf.wi, keep_e, sf.seeds[0], seed_device=sf.seed_device)
+        self.last_embed = dict(keep=keep_e, seed=sf.seed_values[0])
         self.ops["initial_node_representations"] = h0
         # propagation (chem_tensorflow_dense.py:312-340)
         T = self.params["num_timesteps"]
-        eng = self._engine("main")
-        self._stage_adjacency(eng)
+        eng = sf.engine
+        sf.stage(eng)
         edge_keep, state_keep = self._path_keeps()
-        seed_p = self._seed()
         W, gru = self.weights, self.weights["node_gru"]
         beta = W["edge_biases"] if self.params["use_edge_bias"] else None
         wts = {"edge_weights": W["edge_weights"], "edge_biases": beta, "gates_kernel": gru["gates_kernel"],
                "gates_bias": gru["gates_bias"], "candidate_kernel": gru["candidate_kernel"],
                "candidate_bias": gru["candidate_bias"]}
-        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=seed_p)
+        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device)
         hT = eng.forward(h0, pack, T, training=True, state_keep=state_keep)
-        self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=seed_p)
+        self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=sf.seed_values[1])
         self.ops["final_node_representations"] = hT
         # heads + btb loss (chem_tensorflow_dense.py:439-516, chem_tensorflow.py:326-421)
         b, v, _ = hT.shape
         o, oe = self.params["output_size"], self.output_size_edges
-        labels = self._head_labels(b, v)
-        count = self._target_count(task_id) if target_count is None else target_count
-        target_num = float(count + SMALL_NUMBER)
         keep_o = self._out_keep()
-        seed_o = self._seed()
-        if self._heads is None:
-            self._heads = OutputHeads(h)
         hl = self._heads_list(task_id)
-        probs, _ = self._heads.forward(hT, h0, hl, labels, keep_o, seed_o, target_num, loss_out=fl.loss)
-        self.last_heads = dict(keep=keep_o, seed=seed_o, target_num=target_num)
+        probs, _ = sf.heads.forward(hT, h0, hl, sf.labels, keep_o, sf.seeds[2], sf.target_num, loss_out=fl.loss,
+                                    seed_device=sf.seed_device)
+        self.last_heads = dict(keep=keep_o, seed=sf.seed_values[2], target_num=sf.target_num_value)
         self.ops["computed_values"] = probs[0].reshape(b, v * o)
         self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
-        _, _, dhT, dh0_heads = self._heads.backward(hT, h0, hl, labels, probs, target_num,
-                                                     dws=[gv[id(w)] for w, _ in hl], dbs=[gv[id(bb)] for _, bb in hl])
+        _, _, dhT, dh0_heads = sf.heads.backward(hT, h0, hl, sf.labels, probs, sf.target_num,
+                                                  dws=[gv[id(w)] for w, _ in hl], dbs=[gv[id(bb)] for _, bb in hl])
         # the path's backward (TF autodiff, chem_tensorflow.py:496)
         eg = {"h0": torch.empty_like(h0), "edge_weights": gv[id(W["edge_weights"])],
               "edge_biases": gv[id(beta)] if beta is not None else None,
@@ -519,14 +692,16 @@ class DenseGGNNChemModel(BtbBatching):
               "candidate_kernel": gv[id(gru["candidate_kernel"])], "candidate_bias": gv[id(gru["candidate_bias"])]}
         eng.backward(dhT, eg)
         # the tables' gradients + IndexedSlices norms (h0 feeds the path and the heads)
-        self._front_end.backward(segs, wi, eg["h0"], keep_e, seed_e, dh0_add=dh0_heads,
-                                 dtables=[gv[id(t)] for t in tables], sq_out=fl.sq)
+        self._front_end.backward(segs, sf.wi, eg["h0"], keep_e, sf.seeds[0], dh0_add=dh0_heads,
+                                 dtables=[gv[id(t)] for t in tables], sq_out=fl.sq, seed_device=sf.seed_device)
+        return probs
 
     def make_optimizer(self) -> ClipAdam:
         """The reference's train step optimizer (chem_tensorflow.py:494-503) over
         ``trainable_variables()``: clip_by_norm(clamp_gradient_norm) + Adam."""
         self.optimizer = ClipAdam(self.trainable_variables(), learning_rate=self.params["learning_rate"],
                                   clamp_gradient_norm=self.params["clamp_gradient_norm"])
+        self._graphs.clear()          # captured steps hold the old slots' addresses
         return self.optimizer
 
     # ------------------------------------------------- checkpoint / evaluation
@@ -697,9 +872,15 @@ class DenseGGNNChemModel(BtbBatching):
                 batch_loss = self.train_step(feed, all_reduce=all_reduce)
             else:
                 feed["out_layer_dropout_keep_prob"] = 1.0
-                self.feed(feed)
-                with torch.no_grad():
-                    batch_loss = self.build_loss()
+                batch_loss = None
+                if self._graph_ok(feed):
+                    with torch.no_grad():
+                        batch_loss = self._graph_step(feed, False)
+                if batch_loss is None:
+                    self.graph_stats["eager"] += 1
+                    self.feed(feed)
+                    with torch.no_grad():
+                        batch_loss = self.build_loss()
             cur = self._fetch_batch(batch_loss, feed)
             # one batch in flight: the host scores batch k while the GPU runs k + 1
             if pending is not None:

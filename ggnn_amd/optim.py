@@ -50,10 +50,13 @@ class ClipAdam:
         self._lib = _lib.load()
 
     @torch.no_grad()
-    def step(self, grads, grad_scale: float = 1.0, sqnorms=None) -> None:
+    def step(self, grads, grad_scale: float = 1.0, sqnorms=None, step_dev=None) -> None:
         """sqnorms: optional list (None entries allowed) of device scalars that
         replace ||grad||^2 in clip_by_norm -- the per-lookup norm of an
-        embedding's IndexedSlices gradient (EmbeddingFrontEnd.backward)."""
+        embedding's IndexedSlices gradient (EmbeddingFrontEnd.backward).
+        step_dev: a device int64 tensor holding the step count to use
+        (ggnn_adam_step_dev, for hipGraph capture); the caller keeps ``t``
+        (it is not advanced here)."""
         grads = list(grads)
         sqnorms = list(sqnorms) if sqnorms is not None else [None] * len(grads)
         if len(grads) != len(self.params):
@@ -65,8 +68,16 @@ class ClipAdam:
             sq = sqnorms[i]
             tab[i] = AdamTensor(p.data_ptr(), g.data_ptr(), self.m[i].data_ptr(), self.v[i].data_ptr(), p.numel(),
                                 None if sq is None else sq.data_ptr())
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if step_dev is not None:
+            if step_dev.dtype != torch.int64 or step_dev.device.type != "cuda":
+                raise ValueError("step_dev must be a device int64 tensor")
+            _lib.check(self._lib.ggnn_adam_step_dev(tab, len(self.params), self.lr, self.b1, self.b2, self.eps,
+                                                    self.clip, ctypes.c_void_p(step_dev.data_ptr()),
+                                                    float(grad_scale), ctypes.c_void_p(self._scratch.data_ptr()),
+                                                    stream), "ggnn_adam_step_dev")
+            return
         self.t += 1
         _lib.check(self._lib.ggnn_adam_step(tab, len(self.params), self.lr, self.b1, self.b2, self.eps, self.clip,
                                             self.t, float(grad_scale), ctypes.c_void_p(self._scratch.data_ptr()),
-                                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                   "ggnn_adam_step")
+                                            stream), "ggnn_adam_step")

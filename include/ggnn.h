@@ -101,6 +101,13 @@ enum {
  * 4 pairs, so the pair buffers hold 4 * b * v rows plus channel padding);
  * ggnn_set_adjacency rejects it. */
 #define GGNN_SPARSE_PAIRS 64
+/* Dropout seeds live in device memory: dims.seed (and the `seed` argument of
+ * ggnn_embed_* / ggnn_heads_*) holds the ADDRESS of a device uint64 that the
+ * kernels read when they run, instead of the seed itself.  A step captured in
+ * a hipGraph then replays with whatever seed the caller wrote there (by a
+ * captured copy) -- no re-capture per training step.  Same masks as passing
+ * that value directly. */
+#define GGNN_SEED_DEVICE 128
 
 typedef struct ggnn_dims {
   int32_t b;     /* graphs in the batch      (placeholders['num_graphs'])   */
@@ -227,6 +234,13 @@ typedef struct ggnn_adam_tensor {
 int ggnn_adam_step(const ggnn_adam_tensor* tensors, int count, float learning_rate,
                    float beta1, float beta2, float epsilon, float clip_norm,
                    int64_t step, float grad_scale, float* scratch, ggnn_stream_t stream);
+/* The same with the step count read from device memory (a device int64,
+ * >= 1) and the bias-corrected step size derived from it in-kernel: a step
+ * captured in a hipGraph replays with whatever count the caller wrote there. */
+int ggnn_adam_step_dev(const ggnn_adam_tensor* tensors, int count, float learning_rate,
+                       float beta1, float beta2, float epsilon, float clip_norm,
+                       const int64_t* step, float grad_scale, float* scratch,
+                       ggnn_stream_t stream);
 
 /* Materialise a dropout keep-mask (1 = kept, 0 = dropped) exactly as the
  * kernels apply it, for verification: kind 0 = edge-weight mask of timestep t
@@ -276,7 +290,9 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
  *   probs = softmax(z) over o                    (computed_values [b, v*o])
  *   loss  = sum_rows -sum_o labels * log(probs) / target_num
  * target_num = sum(target_mask[task]) + SMALL_NUMBER (the caller's host
- * value).  One mask per head per step (keep, seed). */
+ * value; the _dev variants below read it from device memory).  One mask per
+ * head per step (keep, seed; GGNN_SEED_DEVICE in d->flags: seed is the
+ * address of a device uint64). */
 typedef struct ggnn_output_head {
   const float* weight; /* MLP_W_layer0 [2h][o] */
   const float* bias;   /* MLP_b_layer0 [o] */
@@ -298,6 +314,16 @@ int ggnn_heads_forward(const ggnn_dims* d, const ggnn_output_head* heads, int nh
 int ggnn_heads_backward(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
                         const float* h0, float target_num, const float* d_loss, void* ws, float* dhT,
                         float* dh0, ggnn_stream_t stream);
+/* The same two with target_num read from device memory (a device float > 0),
+ * for hipGraph capture of a training step: identical results to passing that
+ * value (the normaliser 1 / target_num and the power-of-two scale of dZ are
+ * derived from it in the kernels). */
+int ggnn_heads_forward_dev(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                           const float* h0, float keep, uint64_t seed, const float* target_num, float* loss,
+                           void* ws, ggnn_stream_t stream);
+int ggnn_heads_backward_dev(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, const float* hT,
+                            const float* h0, const float* target_num, const float* d_loss, void* ws,
+                            float* dhT, float* dh0, ggnn_stream_t stream);
 
 /* Optional per-kernel timing (HIP events around every launch of the library
  * on the launch's stream), used by bench.py for the roofline.  Not for use

@@ -1,0 +1,140 @@
+"""hipGraph-captured steps (ggnn_amd/graphs.py) against the eager path.
+
+The captured step reads its batch and its step scalars (dropout seeds,
+target_num, Adam step) from device memory and replays the same launches; on
+the same inputs and seeds it must give the eager step's results.  The
+library's split-K weight gradients accumulate with fp32 atomics, so two runs
+of either path agree to rounding, not bit for bit: the first step's forward
+is compared exactly, its gradients and Adam slots at 1e-5 / 1e-4 relative
+(max-norm), later steps within the drift Adam makes of rounding noise.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _model(graphs, lr=None):
+    from ggnn_amd.batching import wsj_model_sizes
+    from ggnn_amd.model import DenseGGNNChemModel
+    params = {"compact_adjacency": True, "hip_graphs": graphs}
+    if lr is not None:
+        params["learning_rate"] = lr
+    return DenseGGNNChemModel(params=params, seed=0, **wsj_model_sizes())
+
+
+def _feeds(m, restrict, training):
+    from ggnn_amd.batching import TRAIN_WITH_DEV
+    np.random.seed(0)
+    data = m.load_data(TRAIN_WITH_DEV["train_file"], training, restrict=restrict)
+    return list(m.make_minibatch_iterator(data, training))
+
+
+def _shape_sequence(feeds):
+    """A batch, the same batch again (new seeds, new weights), a batch of
+    another shape, the first again: capture, replay, second capture, replay."""
+    a = feeds[0]
+    other = next(f for f in feeds if (f["num_graphs"], f["num_vertices"]) != (a["num_graphs"], a["num_vertices"]))
+    return [a, a, other, a]
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+def test_captured_train_steps_match_eager():
+    torch = _torch()
+    ea, gr = _model(False), _model(True)
+    seq = _shape_sequence(_feeds(ea, 100, True))
+    for k, f in enumerate(seq):
+        w0 = [p.detach().clone() for p in gr.trainable_variables()]
+        la = float(ea.train_step(dict(f)))
+        pa = ea.ops["computed_values"].clone()
+        lb = float(gr.train_step(dict(f)))
+        torch.cuda.synchronize()
+        flat_rel = _rel(gr.train_buffer().flat, ea.train_buffer().flat)
+        if k == 0:
+            # same weights, inputs and seeds: the forward is deterministic, the
+            # gradients agree to the atomics' rounding
+            assert la == lb
+            assert torch.equal(pa, gr.ops["computed_values"])
+            assert flat_rel <= 1e-5
+            for ma, mb in zip(ea.optimizer.m + ea.optimizer.v, gr.optimizer.m + gr.optimizer.v):
+                assert _rel(mb, ma) <= 1e-4
+        else:
+            # Adam's first step moves every weight by ~lr whatever its gradient's
+            # size, so elements whose gradient is rounding noise differ by
+            # ~2 lr between any two runs: later steps agree to that drift
+            assert abs(la - lb) <= 1e-4 * abs(la)
+            assert float((pa - gr.ops["computed_values"]).abs().max()) <= 1e-4
+            assert flat_rel <= 2e-3
+        # the Adam step (device step count): the same update on all but a few
+        # near-zero-gradient elements
+        for pe, pg, p0 in zip(ea.trainable_variables(), gr.trainable_variables(), w0):
+            de, dg = (pe.detach() - p0).double(), (pg.detach() - p0).double()
+            close = ((de - dg).abs() <= 1e-6 + 1e-2 * de.abs()).double().mean()
+            assert float(close) >= (0.999 if k == 0 else 0.99)
+        assert ea.optimizer.t == gr.optimizer.t == k + 1
+    st = gr.graph_stats
+    assert st["captured"] == 2 and st["replayed"] == 2 and st["eager"] == 0, st
+    assert ea.graph_stats["eager"] == len(seq)
+
+
+def test_captured_eval_matches_eager():
+    torch = _torch()
+    ea, gr = _model(False), _model(True)
+    from ggnn_amd.batching import TRAIN_WITH_DEV
+    valid = ea.load_data(TRAIN_WITH_DEV["valid_file"], False, restrict=150)
+    ra = ea.run_epoch("valid", valid, False)
+    for _ in range(2):               # first pass captures, second replays
+        rb = gr.run_epoch("valid", valid, False)
+        torch.cuda.synchronize()
+        assert abs(ra[0] - rb[0]) <= 1e-6 * abs(ra[0])
+        assert ra[5] == rb[5] and ra[6] == rb[6] and ra[16] == rb[16]
+        for xa, xb in zip(ra[8], rb[8]):
+            assert np.array_equal(xa, xb)            # computed_values: forward only, deterministic
+    assert gr.graph_stats["replayed"] > 0
+
+
+def test_captured_run_epoch_trains_like_eager():
+    """Two training epochs through captured steps follow the eager run (loss
+    and LAS within the drift of fp32 atomics over ~20 Adam steps)."""
+    _torch()
+    from ggnn_amd.batching import TRAIN_WITH_DEV
+    ea, gr = _model(False), _model(True)
+    # (one copy of the data per model: run_epoch shuffles its buckets in place)
+    np.random.seed(0)
+    train_a = ea.load_data(TRAIN_WITH_DEV["train_file"], True, restrict=200)
+    np.random.seed(0)
+    train_b = gr.load_data(TRAIN_WITH_DEV["train_file"], True, restrict=200)
+    for epoch in range(2):
+        np.random.seed(epoch + 1)
+        ra = ea.run_epoch("e", train_a, True)
+        np.random.seed(epoch + 1)
+        rb = gr.run_epoch("g", train_b, True)
+        assert abs(ra[0] - rb[0]) <= 2e-3 * abs(ra[0])
+        assert abs(ra[5] - rb[5]) <= 0.02
+    st = gr.graph_stats
+    assert st["replayed"] > 0 and st["eager"] == 0
+
+
+def test_profiler_sees_no_capture():
+    """The kernel timer skips records while a stream is capturing (a timed
+    epoch with graphs on still completes and times its eager launches)."""
+    torch = _torch()
+    from ggnn_amd import _lib
+    gr = _model(True)
+    feeds = _feeds(gr, 60, True)
+    with _lib.KernelTimer(max_launches=100000) as t:
+        for f in feeds[:3]:
+            gr.train_step(dict(f))
+        torch.cuda.synchronize()
+    assert sum(t.launches.values()) > 0
