@@ -446,32 +446,61 @@ def end_to_end_side(dev, rank=0, world=1, epochs=1, restrict=True):
     buffer per global step), so the value is the N-rank job's instances/sec.
     restrict: also the README's sample run (--restrict_data 100, epoch 1 of a
     fresh model, train + valid; README.md:25-43)."""
+    from ggnn_amd import _lib
     from ggnn_amd.batching import TRAIN_WITH_DEV, wsj_model_sizes
     from ggnn_amd.model import DenseGGNNChemModel
 
-    def fresh():
+    def fresh(graphs=True):
         np.random.seed(0)                      # chem_tensorflow.py:175
-        return DenseGGNNChemModel(params={"compact_adjacency": True}, seed=0, device=dev, rank=rank,
-                                  world_size=world, **wsj_model_sizes())
+        return DenseGGNNChemModel(params={"compact_adjacency": True, "hip_graphs": graphs}, seed=0, device=dev,
+                                  rank=rank, world_size=world, **wsj_model_sizes())
 
     m = fresh()
     t0 = time.perf_counter()
     train = m.load_data(TRAIN_WITH_DEV["train_file"], True)
     valid = m.load_data(TRAIN_WITH_DEV["valid_file"], False)
     load_s = time.perf_counter() - t0
-    m.run_epoch("warm-up", train, True)
+    # warm-up: every shape's first batch runs eagerly, its second is captured
+    # (ggnn_amd/graphs.py); a training run of the reference's 200 epochs is
+    # in this steady state from epoch 2 on
+    for _ in range(2):
+        m.run_epoch("warm-up", train, True)
+        m.run_epoch("warm-up", valid, False)
     res = {"params": {k: m.params[k] for k in ("hidden_size", "num_timesteps", "batch_size")},
            "data": "WSJ std->nivre btb, --train_with_dev: train = std dev (1700 sentences), valid = std test (2416)",
-           "n_ranks": world, "load_and_process_s": load_s, "epochs": []}
+           "n_ranks": world, "load_and_process_s": load_s, "epochs": [],
+           "step": "hipGraph-captured per batch shape (one H2D copy + one graph launch per batch; "
+                   "all-reduce and Adam eager when n_ranks > 1)"}
     for e in range(epochs):
+        s0 = dict(m.graph_stats)
         tr = m.run_epoch("train", train, True)
+        s1 = dict(m.graph_stats)
         va = m.run_epoch("valid", valid, False)
+        s2 = dict(m.graph_stats)
         res["epochs"].append({"train_instances_per_sec": tr[3], "train_steps": tr[4], "train_loss": tr[0],
                               "train_las": tr[5], "train_uas": tr[6], "train_uas_e": tr[16],
                               "valid_instances_per_sec": va[3], "valid_loss": va[0], "valid_las": va[5],
-                              "valid_uas": va[6], "valid_uas_e": va[16]})
+                              "valid_uas": va[6], "valid_uas_e": va[16],
+                              "train_batches_by_path": {k: s1[k] - s0[k] for k in s0},
+                              "valid_batches_by_path": {k: s2[k] - s1[k] for k in s1}})
     res.update({k: res["epochs"][-1][k] for k in ("train_instances_per_sec", "valid_instances_per_sec",
                                                    "valid_las", "valid_uas")})
+    # the same epochs on the eager path (every library call launched from the
+    # host): the graphs' gain, and the launches per batch they replace
+    me = fresh(graphs=False)
+    np.random.seed(1)
+    train_e = me.load_data(TRAIN_WITH_DEV["train_file"], True)
+    valid_e = me.load_data(TRAIN_WITH_DEV["valid_file"], False)
+    timer = _lib.KernelTimer(max_launches=400000)
+    with timer:
+        wt = me.run_epoch("warm-up", train_e, True)
+        wv = me.run_epoch("warm-up", valid_e, False)
+    tr_e = me.run_epoch("train", train_e, True)
+    va_e = me.run_epoch("valid", valid_e, False)
+    res["eager_step"] = {"train_instances_per_sec": tr_e[3], "valid_instances_per_sec": va_e[3],
+                         "library_launches_per_batch": sum(timer.launches.values()) / max(wt[4] + wv[4], 1),
+                         "note": "params['hip_graphs'] = False; launches counted over one train + one valid "
+                                 "epoch (kernels, fills and copies of libggnn; plus the host-side uploads)"}
     if restrict:
         # README.md:25-43's sample run: --restrict_data 100 (100 sentences per
         # split: small bucketed batches), epoch 1 of a fresh model (cold: the

@@ -5,7 +5,8 @@ here the eager step is ~85 library launches (front-end, adjacency staging,
 weight pack, T-step forward, heads, the backward of each, clip + Adam), and at
 the reference's batch_size 20 the host's launch work is close to the GPU time.
 A captured step replaces them with one H2D copy of the batch's inputs and one
-graph launch.
+graph launch.  A shape's first batch runs the same body eagerly (one-off
+shapes never pay for a capture); its second batch is captured and replayed.
 
 What stays fixed across replays of one graph (its key: batch shape (b, v),
 the word_inputs width, the dropout keep probabilities, train / eval): every
@@ -136,7 +137,7 @@ class CapturedStep:
         self.heads = heads
         self.graph = None
         self.out = None
-        self.replays = 0
+        self.runs = 0               # batches this step has run (eager first, then replays)
 
 
 def edge_arrays(graphs, v: int, num_edge_types: int):

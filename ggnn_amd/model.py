@@ -212,7 +212,9 @@ class DenseGGNNChemModel(BtbBatching):
         self._flat = None
         self._graphs = {}           # hipGraph-captured steps by batch shape (graphs.py)
         self._ring = None
-        self.graph_stats = {"captured": 0, "replayed": 0, "eager": 0}
+        # batches by path: captured-step replays, first batches of a shape
+        # (eager, on the step's device inputs), the plain eager path
+        self.graph_stats = {"captured": 0, "replayed": 0, "uncaptured": 0, "eager": 0}
         self.lookup_sqnorm = {}
         self.optimizer = None
 
@@ -475,14 +477,13 @@ class DenseGGNNChemModel(BtbBatching):
 
     def _graph_step(self, feed, training, task_id=0, target_count=None, all_reduce=None, grad_scale=1.0):
         """One batch through its shape's captured step: stage the batch's
-        inputs (one H2D copy), then replay the graph -- or, the first time a
-        shape is seen, run the step's body eagerly on the same device inputs
-        and capture it for the next batches of that shape.  Training: the
+        inputs (one H2D copy), then replay the shape's graph.  Training: the
         train_step body (+ clip + Adam inside the graph when there is no
         all-reduce; otherwise the all-reduce and Adam follow eagerly).
         Evaluation: the build_loss forward.  Returns the loss (device
         scalar), or None when the batch does not fit a captured step (more
-        edges than the b * v capacity)."""
+        edges than the b * v capacity).  A shape's first batch runs the body
+        eagerly; its second is captured and replayed; later ones replay."""
         self.feed(feed)
         self._check_front_end_width()
         ph = self.placeholders
@@ -550,18 +551,22 @@ class DenseGGNNChemModel(BtbBatching):
                 probs, loss = self._forward_eval(sf, task_id)
             return {"loss": loss, "probs": probs}
 
-        if cs.graph is None:
-            out = body()                     # the real step for this batch
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                cs.out = body()              # recorded, not executed
-            cs.graph = g
-            self.graph_stats["captured"] += 1
+        if cs.graph is None and cs.runs == 0:
+            # a shape's first batch runs eagerly (on the same device inputs):
+            # one-off shapes never pay for a capture
+            out = body()
+            self.graph_stats["uncaptured"] += 1
         else:
+            if cs.graph is None:             # its second batch: capture, then replay
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    cs.out = body()          # recorded, not executed
+                cs.graph = g
+                self.graph_stats["captured"] += 1
             cs.graph.replay()
-            cs.replays += 1
             out = cs.out
             self.graph_stats["replayed"] += 1
+        cs.runs += 1
         probs = out["probs"]
         self.ops["computed_values"] = probs[0].reshape(b, v * o)
         self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)

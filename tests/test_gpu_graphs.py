@@ -39,10 +39,11 @@ def _feeds(m, restrict, training):
 
 def _shape_sequence(feeds):
     """A batch, the same batch again (new seeds, new weights), a batch of
-    another shape, the first again: capture, replay, second capture, replay."""
+    another shape, the first again, the second again: eager first run,
+    capture + replay, eager first run, replay, capture + replay."""
     a = feeds[0]
     other = next(f for f in feeds if (f["num_graphs"], f["num_vertices"]) != (a["num_graphs"], a["num_vertices"]))
-    return [a, a, other, a]
+    return [a, a, other, a, other]
 
 
 def _rel(a, b):
@@ -84,7 +85,7 @@ def test_captured_train_steps_match_eager():
             assert float(close) >= (0.999 if k == 0 else 0.99)
         assert ea.optimizer.t == gr.optimizer.t == k + 1
     st = gr.graph_stats
-    assert st["captured"] == 2 and st["replayed"] == 2 and st["eager"] == 0, st
+    assert st["captured"] == 2 and st["replayed"] == 3 and st["uncaptured"] == 2 and st["eager"] == 0, st
     assert ea.graph_stats["eager"] == len(seq)
 
 
@@ -94,7 +95,7 @@ def test_captured_eval_matches_eager():
     from ggnn_amd.batching import TRAIN_WITH_DEV
     valid = ea.load_data(TRAIN_WITH_DEV["valid_file"], False, restrict=150)
     ra = ea.run_epoch("valid", valid, False)
-    for _ in range(2):               # first pass captures, second replays
+    for _ in range(3):               # first pass eager, second captures, third replays
         rb = gr.run_epoch("valid", valid, False)
         torch.cuda.synchronize()
         assert abs(ra[0] - rb[0]) <= 1e-6 * abs(ra[0])
