@@ -68,11 +68,11 @@ struct Prof {
       if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
       idx = g_prof.used++;
       g_prof.kind[idx] = k;
-      hipEventRecord(g_prof.ev[2 * idx], s);
+      (void)hipEventRecord(g_prof.ev[2 * idx], s);
     }
   }
   ~Prof() {
-    if (idx >= 0) hipEventRecord(g_prof.ev[2 * idx + 1], s);
+    if (idx >= 0) (void)hipEventRecord(g_prof.ev[2 * idx + 1], s);
   }
 };
 
@@ -719,7 +719,7 @@ const char* ggnn_kernel_kind_name(int kind) {
 int ggnn_profile_begin(int max_launches) {
   if (max_launches < 1) return fail(GGNN_EINVAL, "profile_begin: max_launches < 1");
   for (hipEvent_t e : g_prof.ev)
-    if (e) hipEventDestroy(e);
+    if (e) (void)hipEventDestroy(e);
   g_prof.ev.assign(2 * (size_t)max_launches, nullptr);
   g_prof.kind.assign(max_launches, 0);
   for (auto& e : g_prof.ev) HIPCHK(hipEventCreate(&e));

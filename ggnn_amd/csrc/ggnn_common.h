@@ -288,6 +288,16 @@ struct Drop {
 };
 DEV uint32_t dkey0(const Drop& d) { return d.kp ? d.kp[0] : d.k0; }
 DEV uint32_t dkey1(const Drop& d) { return d.kp ? d.kp[1] : d.k1; }
+// the Drop a kernel works with: a device-resident key loaded once at kernel
+// entry; the copy's kp is a known null, so dkey* fold to k0 / k1 in its loops
+DEV Drop drop_resolve(Drop d) {
+  if (d.kp) {
+    d.k0 = d.kp[0];
+    d.k1 = d.kp[1];
+  }
+  d.kp = nullptr;
+  return d;
+}
 DEV uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {

@@ -62,6 +62,7 @@ struct FusedFwdArgs {
 // rounding points as the unfused k_prop_fwd + k_gru_fwd path: h, M, X, r*h)
 template <int PREC>
 __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
+  const Drop sd = drop_resolve(a.sd);  // (a device-resident key: loaded once)
   using namespace gru2;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   // chunk -> ring slot / image limbs
@@ -390,11 +391,11 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
           const float u = au[rt][r];
           const float hprev = hp[rt][r];
           float x = u * hprev + (1.0f - u) * cc;
-          if (a.sd.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
+          if (sd.thr) {  // DropoutWrapper state dropout of the new state (chem_tensorflow_dense.py:239-240)
             if ((r & 3) == 0) {
-              dw = state_words(a.sd, g, rt * 32 + acc_row0(r) + 4 * hh, n, t);
+              dw = state_words(sd, g, rt * 32 + acc_row0(r) + 4 * hh, n, t);
             }
-            x = drop_apply(a.sd, u4_get(dw, r & 3), x);
+            x = drop_apply(sd, u4_get(dw, r & 3), x);
           }
           hn[r] = x;
           bst(ho, x, vo, so);

@@ -222,6 +222,7 @@ DEV void gg_store(char* hi, char* lo, const float* x, int tid) {
 // WM x WN accumulators per wave: block tile (64 WM) x (64 WN), 4 waves in 2 x 2
 template <int PREC, bool A16, bool AKC, bool BKC, int WM, int WN>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
+  const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gg;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int BMt = 64 * WM, BNt = 64 * WN;
@@ -341,12 +342,12 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm * 32 * WM + 32 * i + acc_row(r, hh);
-            if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
+            if (dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, a.drop_t);  // rows m .. m + 3
             if (m >= a.M) continue;
             float x = gs.alpha * acc[i][j][r] + bn;
             if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
             else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-            if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);
+            if (dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
             const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
             if (a.E) x *= a.E[doff];
             cs += x;

@@ -84,6 +84,7 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
 // A bytes on padding rows; k-contiguous A only)
 template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT>
 __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
+  const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   static_assert(!A16 || AKC, "16-bit A operands are k-contiguous");
@@ -297,12 +298,12 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
-          if (a.dr.thr && (r & 3) == 0) dq = edge_words(a.dr, zp, m, n, a.drop_t);  // rows m .. m + 3
+          if (dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, a.drop_t);  // rows m .. m + 3
           if (m >= a.M) continue;
           float x = gs.alpha * acc[i][j][r] + bn;
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-          if (a.dr.thr) x = drop_apply(a.dr, u4_get(dq, r & 3), x);
+          if (dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
           const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
           if (a.E) x *= a.E[doff];
           cs += x;

@@ -93,6 +93,7 @@ __global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C,
 // being the words of one Philox block.
 // dW[c][i][j] += mask_t / keep * G[c][i][j]   (edge dropout backward, one timestep)
 __global__ void k_gen_wmask_acc(const float* __restrict__ G, float* __restrict__ dW, int C, int H, int t, Drop dr) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   const int HQ = (H + 3) / 4;
   const long total = (long)C * HQ * H;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -138,6 +139,7 @@ DEV bool quad_idx(long q, int H, int v, long b, QuadIdx& x) {
 // h' = u h + (1 - u) c, then the DropoutWrapper state dropout of timestep t
 __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict__ h, const float* __restrict__ cc,
                             float* __restrict__ hout, long N, int H, int v, Drop sd, int t) {
+  sd = drop_resolve(sd);  // (a device-resident key: loaded once)
   const long b = N / v, total = b * ((v + 3) >> 2) * H;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     QuadIdx x;
@@ -209,6 +211,7 @@ __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh,
 // gradient unscale on the last step, else 1)
 __global__ void k_gen_delta(const float* __restrict__ DXH, float* __restrict__ out, long N, int H, int v, Drop sd,
                             int tm, const uint32_t* __restrict__ gmax, int unscale) {
+  sd = drop_resolve(sd);  // (a device-resident key: loaded once)
   const long b = N / v, total = b * ((v + 3) >> 2) * H;
   const float osc = unscale ? gunscale(gmax) : 1.0f;
   const bool drop = sd.thr && tm >= 0;
@@ -230,6 +233,7 @@ __global__ void k_gen_delta(const float* __restrict__ DXH, float* __restrict__ o
 // dL/dh_T staging: delta = S * dL/dh_T (gradient scale), state dropout of T-1
 __global__ void k_gen_delta0(const float* __restrict__ dhT, float* __restrict__ out, long N, int H, int v, Drop sd,
                              int tm, const uint32_t* __restrict__ gmax) {
+  sd = drop_resolve(sd);  // (a device-resident key: loaded once)
   const long b = N / v, total = b * ((v + 3) >> 2) * H;
   const float sc = gscale(gmax);
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {

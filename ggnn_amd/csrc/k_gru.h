@@ -43,6 +43,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
           const float* __restrict__ bc, long wlo_g, long wlo_c, float* __restrict__ hf_out, u16* __restrict__ hb_out,
           u16* __restrict__ hT_out, float* __restrict__ r_out, float* __restrict__ u_out,
           float* __restrict__ c_out, u16* __restrict__ rhT_out, long N, Drop dr, int t, int vsh) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, NT = 64 * NS, KS = H / 16, R = 32 * RT, HCH = H / 8, KSG = 2 * KS;
   typedef Swz<HCH> SH;

@@ -66,6 +66,7 @@ k_gru_fwd2(const float* __restrict__ Xa, const float* __restrict__ hf, const u16
            long wlo_c, float* __restrict__ hf_out, u16* __restrict__ hT_out, float* __restrict__ r_out,
            float* __restrict__ u_out, float* __restrict__ c_out, u16* __restrict__ rhT_out, long N, Drop dr, int t,
            int vsh) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   using namespace gru2;
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 4 * SLOT];
   char* img_hi = smem;

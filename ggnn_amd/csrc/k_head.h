@@ -44,13 +44,14 @@ DEV int emb_find(const EmbArgs& a, int k) {
 // h0 [rows][H]: one thread per (row quad, column): one Philox block serves
 // the quad's 4 rows (its 4 words are the 4 rows' masks)
 __global__ void __launch_bounds__(256) k_embed_fwd(EmbArgs a, const int* __restrict__ wi, float* __restrict__ h0) {
+  const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   const long nq = (a.rows + 3) >> 2, total = nq * a.H;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long q = e / a.H;
     const int k = (int)(e % a.H);
     const int s = emb_find(a, k);
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if (s >= 0 && a.dr.thr) w = emb_words(a.dr, q * 4, k);
+    if (s >= 0 && dr.thr) w = emb_words(dr, q * 4, k);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const long r = q * 4 + i;
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) k_embed_fwd(EmbArgs a, const int* __restr
         const EmbSeg& S = a.s[s];
         const int id = wi[r * a.ncols + S.column];
         if (id >= 0 && id < S.rows) x = S.table[(long)id * S.width + (k - S.offset)];
-        if (a.dr.thr) x = drop_apply(a.dr, u4_get(w, i), x);
+        if (dr.thr) x = drop_apply(dr, u4_get(w, i), x);
       }
       h0[r * a.H + k] = x;
     }
@@ -79,6 +80,7 @@ struct EmbGrad {
 __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const int* __restrict__ wi,
                                                    const float* __restrict__ dh0, const float* __restrict__ dh0_add,
                                                    float* __restrict__ sq) {
+  const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   float acc[EMB_MAXSEG];
 #pragma unroll
   for (int i = 0; i < EMB_MAXSEG; ++i) acc[i] = 0.f;
@@ -89,14 +91,14 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
     const int s = emb_find(a, k);
     if (s < 0) continue;
     const EmbSeg& S = a.s[s];
-    const uint4 w = a.dr.thr ? emb_words(a.dr, q * 4, k) : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 w = dr.thr ? emb_words(dr, q * 4, k) : make_uint4(0u, 0u, 0u, 0u);
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const long r = q * 4 + i;
       if (r >= a.rows) break;
       float g = dh0[r * a.H + k] + (dh0_add ? dh0_add[r * a.H + k] : 0.f);
-      if (a.dr.thr) g = drop_apply(a.dr, u4_get(w, i), g);
+      if (dr.thr) g = drop_apply(dr, u4_get(w, i), g);
       const int id = wi[r * a.ncols + S.column];
       if (id < 0 || id >= S.rows) continue;
       atomicAdd(gd.dtable[s] + (long)id * S.width + (k - S.offset), g);
@@ -133,6 +135,7 @@ DEV uint4 head_words(const Drop& d, int hd, int i, int j) {
 __global__ void k_head_wdrop(const float* __restrict__ W, const float* __restrict__ bias, int K, int o, int op, int Ot,
                              int off, int hd, Drop dr, float* __restrict__ Wd, float* __restrict__ S,
                              float* __restrict__ ball) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   const long total = (long)K * op;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int i = (int)(e / op), j = (int)(e % op);

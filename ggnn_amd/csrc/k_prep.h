@@ -15,6 +15,7 @@
 template <bool F16>
 __global__ void k_pack_B(const float* __restrict__ S, int ldS, long sS, int K, int N, int trans,
                          u16* __restrict__ out, long sO, long lo_off, Drop dr, int t) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   const int total = (N / 32) * (K / 16) * 64;
   const float* Sb = S + sS * blockIdx.y;
   u16* ob = out + sO * blockIdx.y;
@@ -158,6 +159,7 @@ __global__ void __launch_bounds__(256) k_prep_adj(const float* __restrict__ A, i
 // dropout mask of timestep t is applied (backward: dL/dh_T -> dL/dh'_{T-1}).
 __global__ void k_pad_state(const float* __restrict__ h0, int vin, int V, int H, float* __restrict__ hf,
                             u16* __restrict__ hb, long N, int f16, Drop dr, int t, const uint32_t* gmax) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   // one thread per (4-row quad, column): V is a multiple of 4, so a quad lies
   // inside one graph and its 4 state-dropout masks are one Philox block
   const long total = N / 4 * H;
@@ -225,6 +227,7 @@ __global__ void __launch_bounds__(256) k_transpose(const TI* __restrict__ in, TO
 // G[t][c][i][j], G = the per-timestep h_t^T dM_{c,t} from k_wgrad.  One thread
 // per 4 consecutive rows i (one Philox draw per timestep).
 __global__ void k_edge_mask_reduce(const float* __restrict__ G, float* __restrict__ dW, int C, int H, int T, Drop dr) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   const long total = (long)C * (H / 4) * H;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const int j = q % H;
@@ -245,6 +248,7 @@ __global__ void k_edge_mask_reduce(const float* __restrict__ G, float* __restric
 // verification: the keep-mask the kernels apply (kind 0: edge [C][H][H] of
 // timestep t; kind 1: state [b][vin][H] of timestep t), 1 = kept
 __global__ void k_dropout_mask(int kind, int C, int H, int b, int vin, int t, Drop dr, uint8_t* __restrict__ m) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   const long total = kind == 0 ? (long)C * H * H : (long)b * vin * H;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const int k = q % H;
@@ -419,6 +423,7 @@ struct PackJobs {
 };
 template <bool F16>
 __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
+  const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   int ji = 0;
   while (ji + 1 < a.count && a.blk_begin[ji + 1] <= (int)blockIdx.x) ++ji;
   const PackJob& J = a.j[ji];
@@ -438,12 +443,12 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     // whose 4 masks are the 4 words of one Philox block
     const int H = J.K, hq = (H + 3) >> 2;
     const int wj = (int)(q % H), iq = (int)((q / H) % hq), c = (int)(q / ((long)H * hq));
-    const uint4 w = edge_words(a.dr, c, 4 * iq, wj, J.t);
+    const uint4 w = edge_words(dr, c, 4 * iq, wj, J.t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (4 * iq + u >= H) break;
       const long e = ((long)c * H + 4 * iq + u) * H + wj;
-      ((float*)J.out)[e] = drop_apply(a.dr, u4_get(w, u), J.S[e]);
+      ((float*)J.out)[e] = drop_apply(dr, u4_get(w, u), J.S[e]);
     }
     return;
   }
@@ -460,13 +465,13 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
   for (int e = 0; e < 8; ++e) x[e] = J.trans ? Sb[(long)n * J.ldS + k0 + e] : Sb[(long)(k0 + e) * J.ldS + n];
   if (J.drop) {
     if (!J.trans) {  // rows k0 .. k0 + 7 of column n: two quads, two Philox blocks
-      const uint4 w0 = edge_words(a.dr, mat, k0, n, J.t), w1 = edge_words(a.dr, mat, k0 + 4, n, J.t);
+      const uint4 w0 = edge_words(dr, mat, k0, n, J.t), w1 = edge_words(dr, mat, k0 + 4, n, J.t);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = drop_apply(a.dr, u4_get(e < 4 ? w0 : w1, e & 3), x[e]);
+      for (int e = 0; e < 8; ++e) x[e] = drop_apply(dr, u4_get(e < 4 ? w0 : w1, e & 3), x[e]);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        x[e] = drop_apply(a.dr, u4_get(edge_words(a.dr, mat, n, k0 + e, J.t), n & 3), x[e]);
+        x[e] = drop_apply(dr, u4_get(edge_words(dr, mat, n, k0 + e, J.t), n & 3), x[e]);
     }
   }
   *(uint4*)(ob + (size_t)r * 8) = pk8<F16>(x);

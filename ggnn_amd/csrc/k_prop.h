@@ -166,6 +166,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
            const int* __restrict__ chl, int chs, const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
            u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
            const uint32_t* __restrict__ gmax) {
+  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
