@@ -173,6 +173,7 @@ __global__ void __launch_bounds__(256) k_gen_bwd1(const float* __restrict__ d, c
   if (k >= H) return;
   const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
   float sc = 0.f, su = 0.f;
+#pragma unroll 4
   for (long row = r0; row < r1; ++row) {
     const long e = row * H + k, g2 = row * 2 * H + H + k;
     const float u = G[g2], c = cc[e], dl = d[e];
@@ -196,6 +197,7 @@ __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh,
   if (k >= H) return;
   const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
   float sr = 0.f;
+#pragma unroll 4
   for (long row = r0; row < r1; ++row) {
     const long e = row * H + k;
     const float r = G[row * 2 * H + k], x = drh[e];

@@ -158,6 +158,77 @@ __global__ void k_pair_fill(const u16* __restrict__ degc, int* __restrict__ pidx
   }
 }
 
+// S5: the backward's reverse gather lists: for every node row r = (g, j) the
+// pair rows p = (g, i, c) with A[g,c,i,j] = 1, in (ascending channel among the
+// graph's occupied ones, ascending i) -- the order k_pair_scatter_dh sums them
+// in.  FILL = false: counts rcnt[r]; FILL = true: rlist[roff[r] ...] after the
+// scan.  A wave per row, its sources by ballots over the staged transpose row.
+// (<= 4 nonzeros per edge, so the lists fit the pair-row capacity.)
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_pair_rev(const u16* __restrict__ AgT, const unsigned char* __restrict__ occ,
+                                                  const int* __restrict__ pidx, int b, int v, int vp, int C,
+                                                  int* __restrict__ rcnt, const int* __restrict__ roff,
+                                                  int* __restrict__ rlist, int cap) {
+  const int lane = threadIdx.x & 63;
+  const long N = (long)b * v;
+  for (long r = blockIdx.x * 4 + (threadIdx.x >> 6); r < N; r += (long)gridDim.x * 4) {
+    const int g = (int)(r / v), j = (int)(r - (long)g * v);
+    long pos = FILL ? roff[r] : 0;
+    int cnt = 0;
+    const unsigned char* og = occ + (long)g * C;
+    for (int cb = 0; cb < C; cb += 64) {
+      // the graph's occupied channels of this block of 64, ascending
+      unsigned long long mc = __ballot(cb + lane < C && og[cb + lane] != 0);
+      while (mc) {
+        const int c = cb + __ffsll((long long)mc) - 1;
+        mc &= mc - 1ull;
+        const u16* arow = AgT + (((long)g * C + c) * v + j) * vp;
+        const int* pc = pidx + (long)c * N + (long)g * v;
+        for (int ib = 0; ib < v; ib += 64) {
+          const int i = ib + lane;
+          const bool nz = i < v && arow[i] != 0;
+          const unsigned long long m = __ballot(nz);
+          if (FILL && nz) {
+            const long q = pos + __popcll(m & ((1ull << lane) - 1ull));
+            if (q < cap) rlist[q] = pc[i];
+          }
+          pos += __popcll(m);
+          cnt += __popcll(m);
+        }
+      }
+    }
+    if (!FILL && lane == 0) rcnt[r] = cnt;
+  }
+}
+// exclusive scan of rcnt[0, N) into roff[0, N] (one block)
+__global__ void __launch_bounds__(1024) k_pair_rev_scan(const int* __restrict__ rcnt, long N, int* __restrict__ roff) {
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  __shared__ int wsum[16];
+  int base = 0;
+  for (long r0 = 0; r0 < N; r0 += 1024) {
+    const long r = r0 + tid;
+    const int x = r < N ? rcnt[r] : 0;
+    int incl = x;  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      woff += u < w ? wsum[u] : 0;
+      tot += wsum[u];
+    }
+    if (r < N) roff[r] = base + woff + incl - x;
+    base += tot;
+    __syncthreads();
+  }
+  if (tid == 0) roff[N] = base;
+}
+
 // F1 (and its recomputation in the backward): Y[p][k] = sum_j A[g,c,i,j] h[g*v+j][k]
 // for every pair row p = (g*v+i, c) of a live tile; padding rows of a live
 // tile get zeros (the products read whole tiles).  One wave per pair row,
@@ -264,45 +335,30 @@ __global__ void __launch_bounds__(256) k_pair_dbeta(const int* __restrict__ poff
 
 // B3: DXH[g*v+j][H + k] += sum over the channels c of g (ascending) and the
 // receivers i of j on c (A[g,c,i,j] = 1, ascending) of dY[pair(g*v+i, c)][k];
-// one wave per source row, the receivers found by ballots over the staged
-// transpose AgT
-__global__ void __launch_bounds__(256) k_pair_scatter_dh(const u16* __restrict__ AgT, const int* __restrict__ chl,
-                                                         const int* __restrict__ pidx, const float* __restrict__ dY,
-                                                         float* __restrict__ DXH, int b, int v, int vp, int C, int H) {
+// one wave per source row walking its reverse list (S5: built once per staged
+// batch, not per timestep)
+__global__ void __launch_bounds__(256) k_pair_scatter_dh(const int* __restrict__ roff, const int* __restrict__ rlist,
+                                                         const float* __restrict__ dY, float* __restrict__ DXH, long N,
+                                                         int H) {
   const int lane = threadIdx.x & 63;
-  const long N = (long)b * v;
   const int nw = gridDim.x * 4;
   for (long r = blockIdx.x * 4 + (threadIdx.x >> 6); r < N; r += nw) {
-    const int g = (int)(r / v), j = (int)(r - (long)g * v);
-    const int* cl = chl + (long)g * (C + 1);
-    const int n = cl[0];
+    const int e0 = roff[r], e1 = roff[r + 1];
     for (int k0 = 0; k0 < H; k0 += 256) {
       const int k = k0 + 4 * lane;
+      if (k >= H) continue;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int u = 0; u < n; ++u) {
-        const int c = cl[1 + u];
-        const u16* arow = AgT + (((long)g * C + c) * v + j) * vp;
-        const int* pc = pidx + (long)c * N + (long)g * v;
-        for (int ib = 0; ib < v; ib += 64) {
-          const int i = ib + lane;
-          unsigned long long m = __ballot(i < v && arow[i] != 0);
-          while (m) {
-            const int ii = ib + __ffsll((long long)m) - 1;
-            m &= m - 1ull;
-            const int p = pc[ii];
-            if (p >= 0 && k < H) {
-              const float4 x = *(const float4*)(dY + (long)p * H + k);
-              acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
-            }
-          }
+      for (int e = e0; e < e1; ++e) {
+        const int p = rlist[e];
+        if (p >= 0) {
+          const float4 x = *(const float4*)(dY + (long)p * H + k);
+          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
         }
       }
-      if (k < H) {
-        float4* d = (float4*)(DXH + r * 2 * H + H + k);
-        float4 o = *d;
-        o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
-        *d = o;
-      }
+      float4* d = (float4*)(DXH + r * 2 * H + H + k);
+      float4 o = *d;
+      o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+      *d = o;
     }
   }
 }
