@@ -69,6 +69,12 @@ GenAdjL gen_adj_layout(const Cfg& c) {
 struct GenWsL {
   size_t hs, X, G, RH, CC, M, Dl, DXH, DZC, DZG, DRH, GW, gmax, total;
   size_t PY, PZ, PDX;  // pair mode: Y = A h, Z = Y W (dY in the backward), dX gathered, [pcap][H] each
+  // (training: Y and dXg keep one slice of cap_tiles * PAIR_TILE rows per
+  // timestep, so dW_c = sum_t mask_t (Y_t^T dXg_t) runs as ONE product after
+  // the timestep loop; WTL: its term lists, every timestep's tiles of a chunk)
+  size_t WTL, pslice;
+  size_t py(int t) const { return PY + (size_t)t * pslice * 4; }
+  size_t pdx(int t) const { return PDX + (size_t)t * pslice * 4; }
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
   size_t hsl(int t) const { return hs + (size_t)t * nh * 4; }
   size_t x(int t) const { return X + (size_t)(t % ns) * nh * 4; }
@@ -95,9 +101,16 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
   L.RH = o;  o += a4 * L.ns;
   L.CC = o;  o += a4 * L.ns;
   if (c.sparse) {
-    L.PY = o;  o += al((size_t)c.pcap * H * 4);
+    const size_t cap_rows = (size_t)(c.pcap / PAIR_TILE) * PAIR_TILE;
+    const int slices = tr ? c.T : 1;
+    L.pslice = cap_rows * H;
+    L.PY = o;  o += al(std::max<size_t>((size_t)c.pcap * H, (size_t)slices * L.pslice) * 4);
     L.PZ = o;  o += al((size_t)c.pcap * H * 4);
-    if (tr) { L.PDX = o; o += al((size_t)c.pcap * H * 4); }
+    if (tr) {
+      L.PDX = o; o += al((size_t)slices * L.pslice * 4);
+      const size_t zw = (c.pcap / PAIR_TILE) / PAIR_CHUNK + c.C;
+      L.WTL = o; o += al(zw * (1 + (size_t)c.T * PAIR_CHUNK) * 4);
+    }
   } else {
     L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
   }
@@ -213,12 +226,16 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else if (A16) return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
     else if (AKC && !BKC) GGR(false, true, false);
     else if (AKC && BKC) GGR(false, true, true);
-    else if (!AKC && !BKC) GGR1(false, false, false, 128);
+    else if (!AKC && !BKC && a.tgroups > 1) {
+      if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, false, false, false, true, 2, 128, true>), grid, dim3(256), 0, s, a, tm, tn);
+      else hipLaunchKernelGGL((k_gemm_ring<PREC, false, false, false, false, 2, 128, true>), grid, dim3(256), 0, s, a, tm, tn);
+    } else if (!AKC && !BKC) GGR1(false, false, false, 128);
     else return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
 #undef GGR
 #undef GGR1
     return GGNN_OK;
   }
+  if (a.tgroups > 1) return fail(GGNN_EUNSUP, "per-timestep term groups need the ring kernel (16-byte aligned operands)");
   // 64 x 64 block tiles: measured faster than the 128 x 64 / 128 x 128
   // variants of k_gemm on every shape tried (tools/gemm_probe.py: 4096^3, the
   // heads' 32768 x {150, 512} x {512, 150, 256}, a per-graph 128 x 256 x 256):
@@ -289,10 +306,12 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
 
 // pair mode, Y = A h over the pair rows (forward F1; recomputed in the backward)
 void gen_pairs_y(const Cfg& c, const GenAdjL& AL, const void* adj, const float* h, float* Y, hipStream_t s) {
-  const unsigned grid = (unsigned)std::min<long>((c.pcap + 3) / 4, 16384);
+  // (rows of whole tiles only: a partial tile past cap_tiles holds no pair)
+  const int rows = AL.cap_tiles * PAIR_TILE;
+  const unsigned grid = (unsigned)std::min<long>((rows + 3) / 4, 16384);
   hipLaunchKernelGGL(k_pair_gather_y, dim3(grid), dim3(256), 0, s, P<const u16>(adj, AL.Ag), P<const int>(adj, AL.prow),
                      P<const int>(adj, AL.ptile), P<const unsigned char>(adj, AL.pmask), h, Y, c.C, c.vin, AL.vp, c.H,
-                     (int)c.pcap);
+                     rows);
 }
 // the per-tile product Z = A_op W_c (forward: A_op = Y, B = W; backward: A_op =
 // dXg, B = W^T): z = 32-row tile, its channel from the one-entry term list
@@ -483,14 +502,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     if (c.sparse) {
       // pair mode (k_pairs.h): Y_t recomputed from the saved h_t, dXg = dX
       // of the pair rows, dbeta, dY = dXg W_c^T, dh += A^T dY, dW_c += Y^T dXg
-      float* PY = P<float>(ws, L.PY);
+      float* PY = P<float>(ws, L.py(t));
       float* PZ = P<float>(ws, L.PZ);
-      float* PDX = P<float>(ws, L.PDX);
+      float* PDX = P<float>(ws, L.pdx(t));
       {
         Prof p(K_PROP_BWD, s);
         gen_pairs_y(c, AL, adj, ht, PY, s);
-        hipLaunchKernelGGL(k_pair_gather_dx, dim3(grid1d(c.pcap * (H / 4))), dim3(256), 0, s,
-                           P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask), DXH, PDX, (int)c.pcap,
+        hipLaunchKernelGGL(k_pair_gather_dx, dim3(grid1d((long)AL.cap_tiles * PAIR_TILE * (H / 4))), dim3(256), 0, s,
+                           P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask), DXH, PDX,
+                           AL.cap_tiles * PAIR_TILE,
                            c.H);
         if (use_bias)
           hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C, 8), dim3(256), 0, s,
@@ -505,20 +525,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
         hipLaunchKernelGGL(k_pair_scatter_dh, dim3((unsigned)std::min<long>((N + 3) / 4, 16384)), dim3(256), 0, s,
                            P<const int>(adj, AL.roff), P<const int>(adj, AL.rlist), PZ, DXH, N, c.H);
       }
-      // dW_c += Y_c^T dXg_c: z = a chunk of <= PAIR_CHUNK tiles of one channel
-      // (zmap), one term per tile, fp32 atomics (a plain read-add-write for a
-      // channel's only chunk measured slower: 96 -> 110 us per launch at the
-      // reference defaults); under edge dropout the mask of timestep t is
-      // applied in the epilogue (no per-timestep slab)
-      GemmArgs a = gg_args();
-      a.A = PY; a.sAm = 1; a.sAk = H; a.sAq = PAIR_TILE * H;
-      a.B = PDX; a.sBk = H; a.sBn = 1; a.sBq = PAIR_TILE * H;
-      a.D = dW; a.sDp = H * H; a.sDm = H; a.sDn = 1; a.mode = GG_ATOMIC;
-      a.tl = P<const int>(adj, AL.wtl); a.ts = 1 + PAIR_CHUNK;
-      a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
-      a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
-      if (c.ed) { a.dr = c.edrop; a.drop_t = t; }
-      if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
+      // (dW_c: after the timestep loop)
     } else {
     // dM[g,c] = A[g,c]^T dX[g] over the non-empty tiles
     {
@@ -567,6 +574,28 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       hipLaunchKernelGGL(k_gen_delta, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
                          c.sdrop, t - 1, gmax, t == 0 ? 1 : 0);
     }
+  }
+  if (c.sparse) {
+    // dW_c = sum_t mask_t (Y_t^T dXg_t), one launch: z = a chunk of <= PAIR_CHUNK
+    // tiles of one channel (zmap) with every timestep's copy of those tiles as
+    // its terms (term q = t * cap_tiles + tile: the slices are cap_tiles tiles
+    // apart); under edge dropout the accumulator is masked and banked at each
+    // timestep's end (GemmArgs::tgroups), so each chunk adds into dW once per
+    // step instead of once per timestep (fp32 atomics: chunks of one channel)
+    {
+      Prof p(K_WGRAD, s);
+      hipLaunchKernelGGL(k_pair_wtl_expand, dim3((unsigned)((AL.zw + 255) / 256)), dim3(256), 0, s,
+                         P<const int>(adj, AL.wtl), AL.zw, c.T, AL.cap_tiles, P<int>(ws, L.WTL));
+    }
+    GemmArgs a = gg_args();
+    a.A = P<float>(ws, L.py(0)); a.sAm = 1; a.sAk = H; a.sAq = PAIR_TILE * H;
+    a.B = P<float>(ws, L.pdx(0)); a.sBk = H; a.sBn = 1; a.sBq = PAIR_TILE * H;
+    a.D = dW; a.sDp = H * H; a.sDm = H; a.sDn = 1; a.mode = GG_ATOMIC;
+    a.tl = P<const int>(ws, L.WTL); a.ts = 1 + (long)c.T * PAIR_CHUNK;
+    a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
+    a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
+    if (c.ed) { a.dr = c.edrop; a.tgroups = c.T; }
+    if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
   }
   // GRU weight gradients over all T*N rows at once: z = (row chunk, timestep),
   // split-K with fp32 atomics; the chunk count is sized for ~1024 workgroups

@@ -80,6 +80,11 @@ struct GemmArgs {
   // and / or scB (bit 1), and alpha = 1 / S
   const float* snum;
   int sdev;
+  // tgroups > 1 (k_gemm_ring only): z's terms form tgroups equal groups, group
+  // k being timestep k: the accumulator is multiplied by the dropout mask dr of
+  // timestep k (not drop_t) at each group's end and banked, so one launch sums
+  // mask_t-weighted products over t (the pair-mode dW over all timesteps)
+  int tgroups;
 };
 
 // exact power of two S <= t carrying the heads' dZ ~ 1/t into the f16 normal

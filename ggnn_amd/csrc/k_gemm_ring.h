@@ -82,7 +82,9 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
 // 1 x 4, 32 x 32 each: products whose M is one small graph's node count, e.g.
 // v = 30 sentence graphs, where a 128-row tile would spend 3/4 of its MFMAs and
 // A bytes on padding rows; k-contiguous A only)
-template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT>
+// TGRP: per-timestep term groups (GemmArgs::tgroups): the accumulator is masked
+// and banked at each group's end, the epilogue stores the bank
+template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT, bool TGRP = false>
 __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gr;
@@ -214,6 +216,14 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
   for (int i = 0; i < AM; ++i)
 #pragma unroll
     for (int j = 0; j < AN; ++j) acc[i][j] = splat(0.f);
+  // TGRP: the masked sum of the finished groups
+  f32x16 bank[TGRP ? AM : 1][TGRP ? AN : 1];
+  if constexpr (TGRP) {
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+      for (int j = 0; j < AN; ++j) bank[i][j] = splat(0.f);
+  }
 
   // ---- MFMAs of the slice in ring slot `buf` (straight-line: the LDS reads
   // of both k-steps issue together)
@@ -262,6 +272,27 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
     }
   };
 
+  // ---- TGRP: group tg (timestep tg) done: bank += mask_tg * acc, acc = 0
+  const int gsz = TGRP ? nit / max(a.tgroups, 1) : 0;
+  auto bank_group = [&](int tg) {
+#pragma unroll
+    for (int j = 0; j < AN; ++j) {
+      const int n = n0 + wn * AN * 32 + 32 * j + l32;
+      uint4 dq = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int i = 0; i < AM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
+          if (dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, tg);  // rows m .. m + 3
+          const float x = acc[i][j][r];
+          bank[i][j][r] += dr.thr ? drop_apply(dr, u4_get(dq, r & 3), x) : x;
+        }
+        acc[i][j] = splat(0.f);
+      }
+    }
+  };
+
   // ---- the ring: slices it+1, it+2 stay in flight while slice it is consumed
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
@@ -276,7 +307,11 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
         if (it + NBUF - 1 < nit) stage(it + NBUF - 1, slot((u + NBUF - 1) % NBUF));
-        if (live) compute(slot(u));
+        if (live) {
+          compute(slot(u));
+          if constexpr (TGRP)
+            if (gsz > 0 && (it + 1) % gsz == 0) bank_group((it + 1) / gsz - 1);
+        }
       }
     }
   }
@@ -298,12 +333,12 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
-          if (dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, a.drop_t);  // rows m .. m + 3
+          if (!TGRP && dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, a.drop_t);  // rows m .. m + 3
           if (m >= a.M) continue;
-          float x = gs.alpha * acc[i][j][r] + bn;
+          float x = gs.alpha * (TGRP ? bank[i][j][r] : acc[i][j][r]) + bn;
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
-          if (dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
+          if (!TGRP && dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
           const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
           if (a.E) x *= a.E[doff];
           cs += x;

@@ -158,6 +158,20 @@ __global__ void k_pair_fill(const u16* __restrict__ degc, int* __restrict__ pidx
   }
 }
 
+// B5: the dW product's term lists over all T timesteps: chunk z's tiles
+// (wtl[z*(1+PAIR_CHUNK)]) repeated per timestep as q = t * cap_tiles + tile,
+// t ascending (groups of equal size: GemmArgs::tgroups)
+__global__ void k_pair_wtl_expand(const int* __restrict__ wtl, int zw, int T, int cap_tiles, int* __restrict__ out) {
+  const int z = blockIdx.x * blockDim.x + threadIdx.x;
+  if (z >= zw) return;
+  const int* q = wtl + (long)z * (1 + PAIR_CHUNK);
+  int* o = out + (long)z * (1 + (long)T * PAIR_CHUNK);
+  const int n = q[0];
+  o[0] = n * T;
+  for (int t = 0; t < T; ++t)
+    for (int e = 0; e < n; ++e) o[1 + t * n + e] = t * cap_tiles + q[1 + e];
+}
+
 // S5: the backward's reverse gather lists: for every node row r = (g, j) the
 // pair rows p = (g, i, c) with A[g,c,i,j] = 1, in (ascending channel among the
 // graph's occupied ones, ascending i) -- the order k_pair_scatter_dh sums them
