@@ -227,6 +227,9 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else if (AKC && !BKC) GGR(false, true, false);
     else if (AKC && BKC) GGR(false, true, true);
     else if (!AKC && !BKC && a.tgroups > 1) {
+      // (a 4-slot ring, three slices in flight at one workgroup per CU, measured
+      // slower for the weight-gradient products: 1.37 -> 1.72 ms at the
+      // reference configuration)
       if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, false, false, false, true, 2, 128, true>), grid, dim3(256), 0, s, a, tm, tn);
       else hipLaunchKernelGGL((k_gemm_ring<PREC, false, false, false, false, 2, 128, true>), grid, dim3(256), 0, s, a, tm, tn);
     } else if (!AKC && !BKC) GGR1(false, false, false, 128);
@@ -333,7 +336,7 @@ int gen_pairs_product(const Cfg& c, const GenAdjL& AL, const void* adj, const fl
 void gen_lists(const Cfg& c, void* adj, hipStream_t s) {
   const GenAdjL L = gen_adj_layout(c);
   const int n = c.b + c.C;
-  hipLaunchKernelGGL(k_gen_lists, dim3((n + 255) / 256), dim3(256), 0, s, P<const unsigned char>(adj, L.occ), c.b,
+  hipLaunchKernelGGL(k_gen_lists, dim3((n + 3) / 4), dim3(256), 0, s, P<const unsigned char>(adj, L.occ), c.b,
                      c.C, (c.flags & GGNN_DENSE_CHANNELS) ? 1 : 0, P<int>(adj, L.chl), P<int>(adj, L.cgl),
                      P<int>(adj, L.cgc), L.nch, L.gch);
 }
@@ -513,7 +516,10 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
                            AL.cap_tiles * PAIR_TILE,
                            c.H);
         if (use_bias)
-          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C, 8), dim3(256), 0, s,
+          // (row slices of >= 16 rows; up to N / 32 of them: a channel may hold every node row)
+          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C,
+                                                (unsigned)std::min<long>(256, std::max<long>(8, (N + 31) / 32))),
+                             dim3(256), 0, s,
                              P<const int>(adj, AL.poff), P<const int>(adj, AL.pcnt), P<const float>(adj, AL.pdeg), PDX,
                              dbeta, c.H);
       }

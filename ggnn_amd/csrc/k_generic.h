@@ -61,30 +61,44 @@ __global__ void __launch_bounds__(256) k_gen_adj_edges(const int* __restrict__ e
 
 // per-graph channel lists chl[g*(C+1)] = (count, channels...) and per-channel
 // graph lists cgl[c*(b+1)] = (count, graphs...) from occ (and cut into chunks, cgc); with dense != 0
-// every tile counts as occupied (GGNN_DENSE_CHANNELS)
-__global__ void k_gen_lists(const unsigned char* __restrict__ occ, int b, int C, int dense, int* __restrict__ chl,
-                            int* __restrict__ cgl, int* __restrict__ cgc, int nch, int gch) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// every tile counts as occupied (GGNN_DENSE_CHANNELS).  One wave per list,
+// compacted 64 entries at a time by ballots (ascending order)
+__global__ void __launch_bounds__(256) k_gen_lists(const unsigned char* __restrict__ occ, int b, int C, int dense,
+                                                   int* __restrict__ chl, int* __restrict__ cgl, int* __restrict__ cgc,
+                                                   int nch, int gch) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const unsigned long long below = (1ull << lane) - 1ull;
   if (t < b) {
     int* o = chl + (long)t * (C + 1);
     int n = 0;
-    for (int c = 0; c < C; ++c)
-      if (dense || occ[(long)t * C + c]) o[1 + n++] = c;
-    o[0] = n;
+    for (int c0 = 0; c0 < C; c0 += 64) {
+      const int c = c0 + lane;
+      const bool f = c < C && (dense || occ[(long)t * C + c]);
+      const unsigned long long m = __ballot(f);
+      if (f) o[1 + n + __popcll(m & below)] = c;
+      n += __popcll(m);
+    }
+    if (lane == 0) o[0] = n;
   } else if (t < b + C) {
     const int c = t - b;
     int* o = cgl + (long)c * (b + 1);
+    int* q = cgc + (long)c * nch * (gch + 1);
     int n = 0;
-    for (int g = 0; g < b; ++g)
-      if (dense || occ[(long)g * C + c]) o[1 + n++] = g;
-    o[0] = n;
-    // the same list in nch chunks of <= gch graphs: cgc[(c*nch + j)*(gch+1)] = (count, graphs...)
-    for (int j = 0; j < nch; ++j) {
-      int* q = cgc + ((long)c * nch + j) * (gch + 1);
-      const int lo = j * gch, cnt = max(0, min(n - lo, gch));
-      q[0] = cnt;
-      for (int e = 0; e < cnt; ++e) q[1 + e] = o[1 + lo + e];
+    for (int g0 = 0; g0 < b; g0 += 64) {
+      const int g = g0 + lane;
+      const bool f = g < b && (dense || occ[(long)g * C + c]);
+      const unsigned long long m = __ballot(f);
+      if (f) {
+        const int idx = n + __popcll(m & below);
+        o[1 + idx] = g;
+        // the same list in nch chunks of <= gch graphs: cgc[(c*nch + j)*(gch+1)] = (count, graphs...)
+        q[(long)(idx / gch) * (gch + 1) + 1 + idx % gch] = g;
+      }
+      n += __popcll(m);
     }
+    if (lane == 0) o[0] = n;
+    for (int j = lane; j < nch; j += 64) q[(long)j * (gch + 1)] = max(0, min(n - j * gch, gch));
   }
 }
 

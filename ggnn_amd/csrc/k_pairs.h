@@ -340,9 +340,10 @@ __global__ void __launch_bounds__(256) k_pair_dbeta(const int* __restrict__ poff
   const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
   if (k >= H) return;
   const int n = pcnt[c], p0 = poff[c];
-  const int per = (n + gridDim.z - 1) / gridDim.z, a = blockIdx.z * per, e = min(n, a + per);
+  const int per = max(16, (n + gridDim.z - 1) / gridDim.z), a = blockIdx.z * per, e = min(n, a + per);
   if (a >= e) return;
   float s = 0.f;
+#pragma unroll 4
   for (int p = p0 + a; p < p0 + e; ++p) s += pdeg[p] * dXg[(long)p * H + k];
   atomicAdd(dbeta + (long)c * H + k, s);
 }
