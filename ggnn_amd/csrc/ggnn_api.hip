@@ -836,7 +836,10 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
   copy(bg, P<float>(pack, L.bg), 2L * H);
   copy(bc, P<float>(pack, L.bc), (long)H);
-  // the general path's fp32 operands (generic_path.h)
+  // the general path's fp32 operands (generic_path.h), also in a pack made for
+  // the specialised kernels: a pack is made with b = v = 1 dims and may serve a
+  // later general-path batch (v > 128).  Measured cost at config 3: 3.5 MB of
+  // copies, the whole pack launch 0.013 ms per step (profiles/r03b_bench.json)
   for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
   copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
   copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
