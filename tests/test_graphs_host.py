@@ -11,7 +11,7 @@ def test_step_layout_fill_places_every_input():
     b, v, ncols, o, oe = 3, 7, 6, 150, 12
     L = StepLayout(b, v, ncols, o, oe)
     for off in (L.wi, L.edges, L.offs, L.yh, L.ye):
-        assert off % 256 == 0 and off >= StepLayout.SCALARS
+        assert off % 64 == 0 and off >= StepLayout.SCALARS
     assert L.wi < L.edges < L.offs < L.yh < L.ye < L.nbytes
     assert L.edge_capacity == b * v
     rng = np.random.default_rng(0)
