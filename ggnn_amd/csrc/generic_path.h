@@ -295,16 +295,22 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
                        P<int>(adj, L.prow), P<float>(adj, L.pdeg));
-    const unsigned rg = (unsigned)std::min<long>((N + 3) / 4, 16384);
-    hipLaunchKernelGGL(k_pair_rev<false>, dim3(rg), dim3(256), 0, s, P<const u16>(adj, L.AgT),
-                       P<const unsigned char>(adj, L.occ), P<const int>(adj, L.pidx), c.b, c.vin, L.vp, c.C,
-                       P<int>(adj, L.rcnt), (const int*)nullptr, (int*)nullptr, (int)c.pcap);
-    hipLaunchKernelGGL(k_pair_rev_scan, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.rcnt), N, P<int>(adj, L.roff));
-    hipLaunchKernelGGL(k_pair_rev<true>, dim3(rg), dim3(256), 0, s, P<const u16>(adj, L.AgT),
-                       P<const unsigned char>(adj, L.occ), P<const int>(adj, L.pidx), c.b, c.vin, L.vp, c.C,
-                       (int*)nullptr, P<const int>(adj, L.roff), P<int>(adj, L.rlist), (int)c.pcap);
   }
   return GGNN_OK;
+}
+// pair mode, the backward's reverse gather lists (k_pair_rev, S5): built by
+// the backward that needs them, so an evaluation batch never pays for them
+void gen_pairs_rev(const Cfg& c, void* adj, hipStream_t s) {
+  const GenAdjL L = gen_adj_layout(c);
+  const long N = (long)c.b * c.vin;
+  const unsigned rg = (unsigned)std::min<long>((N + 3) / 4, 16384);
+  hipLaunchKernelGGL(k_pair_rev<false>, dim3(rg), dim3(256), 0, s, P<const u16>(adj, L.AgT),
+                     P<const unsigned char>(adj, L.occ), P<const int>(adj, L.pidx), c.b, c.vin, L.vp, c.C,
+                     P<int>(adj, L.rcnt), (const int*)nullptr, (int*)nullptr, (int)c.pcap);
+  hipLaunchKernelGGL(k_pair_rev_scan, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.rcnt), N, P<int>(adj, L.roff));
+  hipLaunchKernelGGL(k_pair_rev<true>, dim3(rg), dim3(256), 0, s, P<const u16>(adj, L.AgT),
+                     P<const unsigned char>(adj, L.occ), P<const int>(adj, L.pidx), c.b, c.vin, L.vp, c.C,
+                     (int*)nullptr, P<const int>(adj, L.roff), P<int>(adj, L.rlist), (int)c.pcap);
 }
 
 // pair mode, Y = A h over the pair rows (forward F1; recomputed in the backward)
@@ -461,6 +467,10 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
                        P<uint32_t>(ws, L.gmax));
     hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
                        gmax);
+  }
+  if (c.sparse) {
+    Prof p(K_PROP_BWD, s);
+    gen_pairs_rev(c, adj, s);
   }
   // The weight gradients take single f16 operands in the fp32-parity mode, as
   // the fast path's k_wgrad256 does (measured <= 3.7e-4 normalised against
