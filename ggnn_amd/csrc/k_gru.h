@@ -227,8 +227,16 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 //   [dX2 | dh2] = dzg @ Wg^T                       (K = 2H)
 //   out: dX^T = (dX1 + dX2)^T, dh + dh2 (fp32)
 // ===========================================================================
+// experiment knob: waves per EU asked of the 32-row (RT = 1) H = 256 variant
+// (4 = two 512-thread workgroups per CU, i.e. <= 128 VGPRs)
+#ifndef GGNN_GB_RT1_WPE
+#define GGNN_GB_RT1_WPE 1
+#endif
+#ifndef GGNN_GB_DU_MEM
+#define GGNN_GB_DU_MEM 0  // delta*u parked in dh_out between phase 1 and 2 instead of registers
+#endif
 template <int H, int RT, int PREC>
-__global__ void __launch_bounds__(2 * H)
+__global__ void __launch_bounds__(2 * H, (RT == 1 && H == 256) ? GGNN_GB_RT1_WPE : 1)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
@@ -258,7 +266,9 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
   float csum = 0.f, usum = 0.f;
-  float du[RT][16];
+  constexpr bool DUM = GGNN_GB_DU_MEM && RT == 1;
+  float du[DUM ? 1 : RT][16];
+  const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
@@ -273,7 +283,8 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         const float d = bld_p<GGNN_GB_AUX>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld_p<GGNN_GB_H_AUX>(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
-        du[rt][4 * q + i] = d * u;
+        if constexpr (DUM) bst(pdo, d * u, vo, so);
+        else du[rt][4 * q + i] = d * u;
         csum += dz[i];
         usum += zu[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
@@ -326,7 +337,10 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         const int so = ro * H * 4;
         const float h = bld_p<GGNN_GB_H_AUX>(ph, vo, so), rr = rq[i];
         const float drh = a2[rt][r];
-        a2[rt][r] = du[rt][r] + drh * rr;
+        float dur;
+        if constexpr (DUM) dur = bld(pdo, vo, so);
+        else dur = du[rt][r];
+        a2[rt][r] = dur + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);
         rsum += zr[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
@@ -355,7 +369,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     }
   });
   TSMARK(1, 4);
-  const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
