@@ -490,13 +490,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       hipLaunchKernelGGL(k_gen_bwd1, ewg, dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)), DZC, DZG, DXH, N,
                          c.H, dbc, dbg);
     }
-    // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k])
-    for (int half = 0; half < 2; ++half) {
+    // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k]), one launch
+    // over both halves: columns n >= H go to d(rh) (a separate [N][H] buffer)
+    {
       GemmArgs a = gg_args();
       a.A = DZC; a.sAm = H; a.sAk = 1;
-      a.B = P<float>(pack, PL.gWc) + half * H * H; a.sBk = 1; a.sBn = H;
-      a.D = half ? DRH : DXH; a.sDm = half ? H : 2 * H; a.sDn = 1;
-      a.M = (int)N; a.N = (int)H; a.K = (int)H;
+      a.B = P<float>(pack, PL.gWc); a.sBk = 1; a.sBn = H;
+      a.D = DXH; a.sDm = 2 * H; a.sDn = 1;
+      a.D2 = DRH; a.Nsplit = (int)H; a.sD2m = H;
+      a.M = (int)N; a.N = (int)(2 * H); a.K = (int)H;
       if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
     }
     {

@@ -56,11 +56,13 @@ struct GemmArgs {
   int epi, mode;
   // row / column splits of one product over two buffers (Msplit, Nsplit
   // multiples of 64; 0 = none): A rows m >= Msplit come from Am2 (row
-  // m - Msplit), outputs n >= Nsplit go to D2 (column n - Nsplit)
+  // m - Msplit), outputs n >= Nsplit go to D2 (column n - Nsplit; row
+  // stride sD2m, or sDm when 0)
   const void* Am2;
   int Msplit;
   float* D2;
   int Nsplit;
+  long sD2m;
   // if set: csum[zp*scp + zq*scq + n] += sum over m of the stored values of
   // column n (e.g. the edge-bias gradient from dM), one atomic per column per
   // wave pair
@@ -353,7 +355,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
             if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
             else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
             if (dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
-            const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+            const long doff = dbase + (long)m * (hi_n && a.sD2m ? a.sD2m : a.sDm) + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
             if (a.E) x *= a.E[doff];
             cs += x;
             float* d = (hi_n ? a.D2 : a.D) + doff;

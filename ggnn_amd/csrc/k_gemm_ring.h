@@ -82,10 +82,16 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
 // 1 x 4, 32 x 32 each: products whose M is one small graph's node count, e.g.
 // v = 30 sentence graphs, where a 128-row tile would spend 3/4 of its MFMAs and
 // A bytes on padding rows; k-contiguous A only)
+#ifndef GGNN_TGRP_WPE
+#define GGNN_TGRP_WPE 2  // waves per EU asked of the term-group variant: two workgroups per CU (238 VGPRs, no AGPRs; 1: 249 + 64 AGPRs, one per CU)
+#endif
+#ifndef GGNN_TGRP_ONESITE
+#define GGNN_TGRP_ONESITE 1
+#endif
 // TGRP: per-timestep term groups (GemmArgs::tgroups): the accumulator is masked
 // and banked at each group's end, the epilogue stores the bank
 template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT, bool TGRP = false>
-__global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
+__global__ void __launch_bounds__(256, TGRP ? GGNN_TGRP_WPE : 1) k_gemm_ring(GemmArgs a, int tm, int tn) {
   const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -297,6 +303,19 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, slot(u));
+  if constexpr (TGRP && NBUF == 2 && GGNN_TGRP_ONESITE) {
+    // one call site of the masked banking (the unrolled slot loop inlined it
+    // twice): the slot is picked at run time
+    for (int it = 0; it < nit; ++it) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
+      if (it + 1 < nit) stage(it + 1, (it & 1) ? s0 : s1);
+      if (live) {
+        compute((it & 1) ? s1 : s0);
+        if (gsz > 0 && (it + 1) % gsz == 0) bank_group((it + 1) / gsz - 1);
+      }
+    }
+  } else
   for (int it0 = 0; it0 < nit; it0 += NBUF) {
 #pragma unroll
     for (int u = 0; u < NBUF; ++u) {
@@ -339,7 +358,7 @@ __global__ void __launch_bounds__(256) k_gemm_ring(GemmArgs a, int tm, int tn) {
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
           if (!TGRP && dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
-          const long doff = dbase + (long)m * a.sDm + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+          const long doff = dbase + (long)m * (hi_n && a.sD2m ? a.sD2m : a.sDm) + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
           if (a.E) x *= a.E[doff];
           cs += x;
           float* d = (hi_n ? a.D2 : a.D) + doff;
