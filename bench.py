@@ -406,6 +406,20 @@ def real_density_side(dev, b=256, v=30, h=256, E=46, T=5, steps=5, both=True):
 
         ms = _timed_events(step, steps)
         r = {"ms_per_step": ms, "graphs_per_s": b / (ms * 1e-3)}
+        if name == "pairs":
+            # the training feed the reference uses: keep 0.9 for both the edge-weight
+            # and the state dropout (chem_tensorflow_dense.py:155-159, 860-861)
+            nd = [0]
+
+            def step_drop(keep=0.9):
+                nd[0] += 1
+                pack = eng.pack_weights(w_d, T=T, edge_keep=keep, seed=nd[0])
+                eng.forward(h0, pack, T, training=True, out=out, state_keep=keep)
+                eng.backward(dhT, gv)
+
+            msd = _timed_events(step_drop, steps)
+            r["training_dropout"] = {"edge_keep": 0.9, "state_keep": 0.9, "ms_per_step": msd,
+                                     "graphs_per_s": b / (msd * 1e-3)}
         if name in ("pairs", "tiles"):
             tf = algo / (ms * 1e-3) / 1e12
             ts = survey / (ms * 1e-3) / 1e12
