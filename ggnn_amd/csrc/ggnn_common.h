@@ -79,7 +79,24 @@ template <bool F16> DEV uint32_t pk(float a, float b) {
   if constexpr (F16) return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));
   else return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
 }
-template <bool F16> DEV uint32_t pk_lo(float a, float b) {
+#ifndef GGNN_LIMB_MIX
+#define GGNN_LIMB_MIX 1
+#endif
+template <bool F16, bool MIX = GGNN_LIMB_MIX> DEV uint32_t pk_lo(float a, float b) {
+  if constexpr (F16 && MIX) {
+    // f16 residuals by v_fma_mix{lo,hi}_f16: f16(x - f32(hi)) in one
+    // instruction per element (x - hi is exact in fp32, then one RNE rounding:
+    // the same bits as the convert / subtract / convert sequence, 3 instead of
+    // 5 instructions per pair; tools/limb_mix_test.hip checks it on the GPU).
+    // MIX = false keeps the convert sequence: k_fwd_fused measured ~1.4 %
+    // slower with the asm pair in its blend (fewer scheduling choices there),
+    // while the ring GEMM and k_prop_bwd gained 1-5 %
+    const uint32_t hi = pk<true>(a, b);
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(a), "v"(hi));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(hi));
+    return lo;
+  }
   const f32x2v v = {a, b};
   f32x2v back;
   if constexpr (F16) back = __builtin_convertvector(__builtin_convertvector(v, f16x2v), f32x2v);
@@ -90,8 +107,19 @@ template <bool F16> DEV uint32_t pk_lo(float a, float b) {
 template <bool F16> DEV frag pk8(const float* x) {
   return make_uint4(pk<F16>(x[0], x[1]), pk<F16>(x[2], x[3]), pk<F16>(x[4], x[5]), pk<F16>(x[6], x[7]));
 }
-template <bool F16> DEV frag pk8_lo(const float* x) {
-  return make_uint4(pk_lo<F16>(x[0], x[1]), pk_lo<F16>(x[2], x[3]), pk_lo<F16>(x[4], x[5]), pk_lo<F16>(x[6], x[7]));
+// one element's f16 residual limb (v_fma_mixlo_f16 under GGNN_LIMB_MIX)
+DEV u16 lo_limb16(float v) {
+  if constexpr (GGNN_LIMB_MIX) {
+    const uint32_t hi = __builtin_bit_cast(u16, (_Float16)v);
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(v), "v"(hi));
+    return (u16)lo;
+  }
+  return to_limb<true>(lo_part<true>(v));
+}
+template <bool F16, bool MIX = GGNN_LIMB_MIX> DEV frag pk8_lo(const float* x) {
+  return make_uint4(pk_lo<F16, MIX>(x[0], x[1]), pk_lo<F16, MIX>(x[2], x[3]), pk_lo<F16, MIX>(x[4], x[5]),
+                    pk_lo<F16, MIX>(x[6], x[7]));
 }
 template <bool F16> DEV float limb_elem(frag f, int j) {
   const uint32_t w = (j < 2) ? f.x : (j < 4) ? f.y : (j < 6) ? f.z : f.w;
@@ -122,11 +150,11 @@ template <bool F16> DEV frag acc_hi(const f32x16& a, int s) {
   for (int j = 0; j < 8; ++j) x[j] = a[8 * s + j];
   return pk8<F16>(x);
 }
-template <bool F16> DEV frag acc_lo(const f32x16& a, int s) {
+template <bool F16, bool MIX = GGNN_LIMB_MIX> DEV frag acc_lo(const f32x16& a, int s) {
   float x[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) x[j] = a[8 * s + j];
-  return pk8_lo<F16>(x);
+  return pk8_lo<F16, MIX>(x);
 }
 
 // D += A*B with the precision policy (split: f16 limbs, 3 products)
@@ -456,5 +484,5 @@ template <int PREC> struct WgradPrec { static constexpr int value = Prec<PREC>::
 template <int PREC, int NCH>
 DEV void img_put(char* hi, char* lo, int row, int e, float v) {
   *(u16*)(hi + Swz<NCH>::eoff(row, e)) = to_limb<Prec<PREC>::f16>(v);
-  if constexpr (Prec<PREC>::split) *(u16*)(lo + Swz<NCH>::eoff(row, e)) = to_limb<true>(lo_part<true>(v));
+  if constexpr (Prec<PREC>::split) *(u16*)(lo + Swz<NCH>::eoff(row, e)) = lo_limb16(v);
 }

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
     const float x[8] = {__uint_as_float(v.a.x), __uint_as_float(v.a.y), __uint_as_float(v.a.z), __uint_as_float(v.a.w),
                         __uint_as_float(v.b.x), __uint_as_float(v.b.y), __uint_as_float(v.b.z), __uint_as_float(v.b.w)};
     st16(hi + off, pk8<F16>(x));
-    if constexpr (SPLIT) st16(lo + off, pk8_lo<true>(x));
+    if constexpr (SPLIT) st16(lo + off, pk8_lo<true, false>(x));
   };
   constexpr int V = 128, VT = 4, ACH = V / 8;
   typedef Swz<ACH> SA;
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       const float4 x0 = *(const float4*)(h0 + row * H + ch * 8), x1 = *(const float4*)(h0 + row * H + ch * 8 + 4);
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
       st16(img_hi + koff(row, ch), pk8<F16>(x));
-      if constexpr (SPLIT) st16(img_lo + koff(row, ch), pk8_lo<true>(x));
+      if constexpr (SPLIT) st16(img_lo + koff(row, ch), pk8_lo<true, false>(x));
     }
   }
   if (nc > 0) glds_tile<ACH, V, NT, GGNN_FUSED_A_AUX>(abuf, ag + (long)chan(0) * V * V, (int)threadIdx.x);
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < VT; ++rt) {
         const frag mh0 = acc_hi<F16>(accm[rt], 0), mh1 = acc_hi<F16>(accm[rt], 1);
-        const frag ml0 = SPLIT ? acc_lo<true>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<true>(accm[rt], 1) : mh1;
+        const frag ml0 = SPLIT ? acc_lo<true, false>(accm[rt], 0) : mh0, ml1 = SPLIT ? acc_lo<true, false>(accm[rt], 1) : mh1;
 #pragma unroll
         for (int it = 0; it < VT; ++it) {
           const frag a0 = lds_frag(abuf, SA::off(it * 32 + l32, 4 * rt + hh));
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
           const v2u32 wh = quad_transpose4(pk<F16>(hn[4 * q], hn[4 * q + 1]), pk<F16>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
           *(uint2*)(img_hi + eo) = make_uint2(wh.x, wh.y);
           if constexpr (SPLIT) {
-            const v2u32 wl = quad_transpose4(pk_lo<true>(hn[4 * q], hn[4 * q + 1]), pk_lo<true>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
+            const v2u32 wl = quad_transpose4(pk_lo<true, false>(hn[4 * q], hn[4 * q + 1]), pk_lo<true, false>(hn[4 * q + 2], hn[4 * q + 3]), l32 & 3);
             *(uint2*)(img_lo + eo) = make_uint2(wl.x, wl.y);
           }
         }
