@@ -576,7 +576,9 @@ def main():
                     help="of the side measurements, only the reference's run_epoch line (every rank; rehearsal)")
     ap.add_argument("--dist-backend", default=None, choices=(None, "nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (default nccl = RCCL; gloo only to rehearse "
-                         "several ranks on one GPU)")
+                         "several ranks on one GPU).  Given explicitly at N = 1 (a one-rank torchrun), the "
+                         "one-rank group is created and the per-step all-reduce runs anyway: the RCCL path "
+                         "of an N-GPU run, executed on one GPU")
     ap.add_argument("--pmc-unfused-leg", action="store_true",
                     help="after the timed work, two steps with the unfused forward (k_prop_fwd + k_gru_fwd), so a "
                          "PMC pass over this command covers those kernels too (tools/profile_round.sh)")
@@ -631,7 +633,7 @@ def main():
         opt.step([grads.views[k] for k in GRAD_ORDER], grad_scale=1.0 / world)
 
     def barrier():
-        if world > 1:
+        if tdist.is_initialized():
             tdist.barrier()
         torch.cuda.synchronize()
 
@@ -666,7 +668,7 @@ def main():
         step(args.dropout_keep)
     barrier()
     dt_drop = (time.perf_counter() - t2) / args.steps
-    if world > 1:
+    if tdist.is_initialized():
         tt = torch.tensor([dt, dt_drop], dtype=torch.float64, device=dev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         dt, dt_drop = float(tt[0].item()), float(tt[1].item())
@@ -761,6 +763,10 @@ def main():
             "roofline": roof,
             "achieved_step_tflops": world * b * fpg / dt / 1e12,
             "kernel_breakdown": breakdown,
+            "all_reduce": {"backend": tdist.get_backend() if tdist.is_initialized() else None,
+                           "bytes_per_step": grads.nbytes,
+                           "note": "one all-reduce of the flat fp32 gradient buffer per step (RCCL = backend "
+                                   "nccl); none without a process group"},
             "ms_per_step_event_instrumented": dt_instr * 1e3,
             "adjacency_feed": feed_cmp,
             "dropout_on": {"edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
@@ -776,7 +782,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if tdist.is_initialized():
         tdist.destroy_process_group()
 
 

@@ -328,7 +328,7 @@ class BtbBatching:
         internal = self.params["task_ids"].index(task_id)
         return float(sum(0.0 if d["labels"][internal] is None else 1.0 for d in elements))
 
-    def make_minibatch_iterator(self, data, is_training, rank=0, world_size=1):
+    def make_minibatch_iterator(self, data, is_training, rank=0, world_size=1, schedule=None):
         """Yields feed dicts keyed by placeholder name (chem_tensorflow_dense.py:792-875).
 
         Data parallel (world_size > 1): every rank computes the same schedule
@@ -338,8 +338,9 @@ class BtbBatching:
         ``global_target_count`` / ``global_num_graphs`` of its global step
         (train_step's loss normaliser; no communication needed).  A rank
         without a batch in the last global step gets a feed with
-        num_graphs == 0 (it still joins the step's all-reduce)."""
-        sched = self.minibatch_schedule(data, is_training)
+        num_graphs == 0 (it still joins the step's all-reduce).  ``schedule``:
+        the epoch's minibatch_schedule, when the caller drew it already."""
+        sched = self.minibatch_schedule(data, is_training) if schedule is None else schedule
         bucket_sizes = data[1]
         if world_size <= 1:
             for bidx, elements in sched:

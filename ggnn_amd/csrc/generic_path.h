@@ -170,27 +170,10 @@ static bool ring_ok(const GemmArgs& a, bool A16, bool AKC, bool BKC) {
 // ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail);
 // thread-local, so a forward / backward on another thread never sees it
 static thread_local int g_gemm_force = 0;
-// GGNN_GEMM_KERNEL=old forces k_gemm everywhere (A/B measurements)
-static int gemm_kernel_env() {
-  static const int v = [] {
-    const char* e = getenv("GGNN_GEMM_KERNEL");
-    return (e && !strcmp(e, "old")) ? 1 : 0;
-  }();
-  return v;
-}
-
 // ring depth: 2 slots (64 KiB: two workgroups per CU) -- measured 1.4-2x
 // faster than a 4-slot ring (one workgroup per CU) on every probe shape
 // (tools/gemm_ring_probe.py): a second workgroup's MFMAs cover one's prologue,
 // barriers and epilogue better than deeper prefetch does.
-// GGNN_RING_SMALL=0 keeps 128-row tiles for small-M products (A/B)
-static int ring_small_env() {
-  static const int v = [] {
-    const char* e = getenv("GGNN_RING_SMALL");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
 
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
@@ -198,13 +181,13 @@ template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
-  if ((g_gemm_force == 2 || (g_gemm_force == 0 && gemm_kernel_env() == 0)) && ring_ok(a, A16, AKC, BKC)) {
+  if (g_gemm_force != 1 && ring_ok(a, A16, AKC, BKC)) {
     // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
     // per-(graph, channel) products of v = 30 sentence graphs), and for
     // products whose 128-row grid would leave most CUs idle (the GRU products
     // of a 20-sentence batch: M ~ 600 rows -> 5 x 7 tiles); 128 otherwise
     const long grid128 = (long)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.Z;
-    const bool small = AKC && (a.M <= 64 || grid128 < 128) && ring_small_env();
+    const bool small = AKC && (a.M <= 64 || grid128 < 128);
     const int bm = small ? 32 : 128;
     const int tn = (a.N + 127) / 128, tm = (a.M + bm - 1) / bm;
     const long nwg = (long)tn * tm * a.Z;

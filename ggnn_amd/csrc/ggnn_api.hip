@@ -276,14 +276,25 @@ int grid1d(long n, int bs = 256) {
   const long g = (n + bs - 1) / bs;
   return (int)std::min<long>(std::max<long>(g, 1), 8192);
 }
-// device-side fill / copy on the stream (kernels: capture-safe, see k_fill)
+// device-side fill / copy on the stream (kernels: capture-safe, see k_fill).
+// GGNN_PROBE_MEMSET_NODES builds the round-2 form (hipMemsetAsync /
+// hipMemcpyAsync, i.e. memset and memcpy nodes under stream capture) for
+// tools/capture_probe.py only; the library never ships it.
 void fill_async(void* p, unsigned char byte, size_t nbytes, hipStream_t s) {
   if (!nbytes) return;
+#ifdef GGNN_PROBE_MEMSET_NODES
+  (void)hipMemsetAsync(p, byte, nbytes, s);  // (an error surfaces at the next LAUNCHCHK)
+  return;
+#endif
   hipLaunchKernelGGL(k_fill, dim3(grid1d((long)((nbytes + 15) / 16))), dim3(256), 0, s, (unsigned char*)p, nbytes,
                      (unsigned)byte);
 }
 void copy_async(float* dst, const float* src, long n, hipStream_t s) {
   if (n <= 0) return;
+#ifdef GGNN_PROBE_MEMSET_NODES
+  (void)hipMemcpyAsync(dst, src, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+  return;
+#endif
   hipLaunchKernelGGL(k_copy32, dim3(grid1d((n + 3) / 4)), dim3(256), 0, s, dst, src, n);
 }
 
@@ -357,7 +368,7 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
   do {                                                                               \
     constexpr bool sp_ = Prec<PREC>::split;                                          \
     constexpr int mx_ = sp_ ? kSplitRT<FN##_tag>::value : kMaxRT<FN##_tag, H>::value; \
-    const int rt_ = std::min(gru_rt(c, mx_), rt_cap<FN##_tag>());                    \
+    const int rt_ = gru_rt(c, mx_);                                                  \
     if (mx_ >= 4 && rt_ == 4) FN<H, mx_ >= 4 ? 4 : 2, PREC>(__VA_ARGS__);            \
     else if (rt_ == 2) FN<H, 2, PREC>(__VA_ARGS__);                                  \
     else FN<H, 1, PREC>(__VA_ARGS__);                                                \
@@ -373,15 +384,6 @@ void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const flo
 // registers) live through both products and spills at RT = 4.
 struct launch_gru_fwd_tag {};
 struct launch_gru_bwd_tag {};
-// GGNN_GRU_BWD_RT caps the GRU backward's row tiles (experiment knob)
-template <typename TAG> int rt_cap() { return 4; }
-template <> int rt_cap<launch_gru_bwd_tag>() {
-  static const int v = [] {
-    const char* e = getenv("GGNN_GRU_BWD_RT");
-    return e ? std::max(1, atoi(e)) : 4;
-  }();
-  return v;
-}
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
 template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
@@ -463,11 +465,6 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     fa.T = c.T;
     fa.vsh = c.vsh;
     fa.sd = c.sdrop;
-    static const int skew = [] {
-      const char* e = getenv("GGNN_FWD_SKEW");
-      return e ? std::max(0, atoi(e)) : 0;
-    }();
-    fa.skew = skew;
     {
       Prof p(K_FWD_FUSED, s);
       hipLaunchKernelGGL(k_fwd_fused<PREC>, dim3(c.b), dim3(512), 0, s, fa);

@@ -24,13 +24,9 @@
 
 #define FUSED_MAXT 16
 // cache policy of the adjacency LDS-DMA: nontemporal (the tiles are read once
-// per timestep; measured -1.5 % on the kernel, less L2 pollution for the X scratch)
-#ifndef GGNN_FUSED_SAVE_NT
-#define GGNN_FUSED_SAVE_NT 0  // nontemporal r / u / c saves: measured no gain, off
-#endif
-#ifndef GGNN_FUSED_A_AUX
-#define GGNN_FUSED_A_AUX kNT
-#endif
+// per timestep; measured -1.5 % on the kernel, less L2 pollution for the X
+// scratch).  (Nontemporal r / u / c saves measured no gain.)
+constexpr int kFusedAAux = kNT;
 struct FusedFwdArgs {
   const u16* Ab;                // staged adjacency [b][C][128][128] (k_prep.h layout)
   const int* chl;               // per-graph non-empty channel lists (k_chan_list), graph stride chs
@@ -54,7 +50,6 @@ struct FusedFwdArgs {
   long sw, s4;
   int C, T, vsh;
   Drop sd;
-  int skew;                     // experiment knob (GGNN_FWD_SKEW): odd graphs start skew x s_sleep(127) late
 };
 
 // PREC: PREC_SPLIT (fp32-parity: f16 hi/lo limb images, 3 products) or a
@@ -82,8 +77,6 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
   auto slot_lo = [&](int u) { return smem + 2 * IMG + u * 2 * SLOT + SLOT; };
 
   const int g = blockIdx.x;
-  if (a.skew && (g & 1))
-    for (int k = 0; k < a.skew; ++k) __builtin_amdgcn_s_sleep(127);
   const long row0 = (long)g * R;
   const int C = a.C;
   const u16* ag = a.Ab + (long)g * C * V * V;
@@ -108,7 +101,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       if constexpr (SPLIT) st16(img_lo + koff(row, ch), pk8_lo<true, false>(x));
     }
   }
-  if (nc > 0) glds_tile<ACH, V, NT, GGNN_FUSED_A_AUX>(abuf, ag + (long)chan(0) * V * V, (int)threadIdx.x);
+  if (nc > 0) glds_tile<ACH, V, NT, kFusedAAux>(abuf, ag + (long)chan(0) * V * V, (int)threadIdx.x);
 
   for (int t = 0; t < a.T; ++t) {
     __syncthreads();  // h_t image complete, A_0 staged (previous blend / prologue)
@@ -181,7 +174,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         }
       }
       __syncthreads();  // S2: A_c reads done
-      if (ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_FUSED_A_AUX>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
+      if (ci + 1 < nc) glds_tile<ACH, V, NT, kFusedAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     }
     TSMARK(2, 1);
     // X -> scratch (accumulator order) and X^T (weight-gradient operand)
@@ -291,7 +284,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         if (a.r) {  // row-quad-major save (ggnn_common.h: qm_vo)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.r + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            gst4(a.r + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]));
         }
         if (rht) {
@@ -365,7 +358,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
     }
     TSMARK(2, 5);
     // next timestep's first adjacency tile lands while the blend runs
-    if (t + 1 < a.T && nc > 0) glds_tile<ACH, V, NT, GGNN_FUSED_A_AUX>(abuf, ag + (long)chan(0) * V * V, tid);
+    if (t + 1 < a.T && nc > 0) glds_tile<ACH, V, NT, kFusedAAux>(abuf, ag + (long)chan(0) * V * V, tid);
 
     // ===================== blend: h' = u h + (1-u) c, state dropout =====================
     {
@@ -405,9 +398,9 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
         if (sav) {  // row-quad-major saves
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.u + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            gst4(a.u + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(uv[4 * q], uv[4 * q + 1], uv[4 * q + 2], uv[4 * q + 3]));
-            (GGNN_FUSED_SAVE_NT ? gst4_nt : gst4)(a.c + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
+            gst4(a.c + t * a.s4 + row0 * H, qm_vo(hh, n, H), qm_so(rt, q, H),
                  make_float4(cv[4 * q], cv[4 * q + 1], cv[4 * q + 2], cv[4 * q + 3]));
           }
         }

@@ -82,16 +82,13 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
 // 1 x 4, 32 x 32 each: products whose M is one small graph's node count, e.g.
 // v = 30 sentence graphs, where a 128-row tile would spend 3/4 of its MFMAs and
 // A bytes on padding rows; k-contiguous A only)
-#ifndef GGNN_TGRP_WPE
-#define GGNN_TGRP_WPE 2  // waves per EU asked of the term-group variant: two workgroups per CU (238 VGPRs, no AGPRs; 1: 249 + 64 AGPRs, one per CU)
-#endif
-#ifndef GGNN_TGRP_ONESITE
-#define GGNN_TGRP_ONESITE 1
-#endif
 // TGRP: per-timestep term groups (GemmArgs::tgroups): the accumulator is masked
-// and banked at each group's end, the epilogue stores the bank
+// and banked at each group's end, the epilogue stores the bank.  It asks for 2
+// waves per EU (two workgroups per CU: 238 VGPRs, no AGPRs; at 1 it held 249 +
+// 64 AGPRs, one workgroup per CU, 1.37 vs 0.95 ms) and banks from ONE call site
+// (the unrolled slot loop inlined it twice).
 template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT, bool TGRP = false>
-__global__ void __launch_bounds__(256, TGRP ? GGNN_TGRP_WPE : 1) k_gemm_ring(GemmArgs a, int tm, int tn) {
+__global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int tm, int tn) {
   const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -303,7 +300,7 @@ __global__ void __launch_bounds__(256, TGRP ? GGNN_TGRP_WPE : 1) k_gemm_ring(Gem
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, slot(u));
-  if constexpr (TGRP && NBUF == 2 && GGNN_TGRP_ONESITE) {
+  if constexpr (TGRP && NBUF == 2) {
     // one call site of the masked banking (the unrolled slot loop inlined it
     // twice): the slot is picked at run time
     for (int it = 0; it < nit; ++it) {

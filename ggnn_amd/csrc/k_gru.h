@@ -13,13 +13,9 @@
 
 // cache policy of k_gru_bwd's saved-activation loads (r, u, c, delta: read
 // once): nontemporal, so they do not evict the Wc^T / Wg^T fragments the
-// products stream from L2 (measured -2.8 % on k_gru_bwd, A/B on one box)
-#ifndef GGNN_GB_AUX
-#define GGNN_GB_AUX kNT
-#endif
-#ifndef GGNN_GB_H_AUX
-#define GGNN_GB_H_AUX 0  // the state h (read in both phases): experiment
-#endif
+// products stream from L2 (measured -2.8 % on k_gru_bwd, A/B on one box); the
+// state h is read in both phases and keeps the default policy
+constexpr int kGbAux = kNT;
 
 // weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
 // full unrolling, which spills at H = 256)
@@ -227,16 +223,8 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 //   [dX2 | dh2] = dzg @ Wg^T                       (K = 2H)
 //   out: dX^T = (dX1 + dX2)^T, dh + dh2 (fp32)
 // ===========================================================================
-// experiment knob: waves per EU asked of the 32-row (RT = 1) H = 256 variant
-// (4 = two 512-thread workgroups per CU, i.e. <= 128 VGPRs)
-#ifndef GGNN_GB_RT1_WPE
-#define GGNN_GB_RT1_WPE 1
-#endif
-#ifndef GGNN_GB_DU_MEM
-#define GGNN_GB_DU_MEM 0  // delta*u parked in dh_out between phase 1 and 2 instead of registers
-#endif
 template <int H, int RT, int PREC>
-__global__ void __launch_bounds__(2 * H, (RT == 1 && H == 256) ? GGNN_GB_RT1_WPE : 1)
+__global__ void __launch_bounds__(2 * H)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
@@ -266,25 +254,23 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
   float csum = 0.f, usum = 0.f;
-  constexpr bool DUM = GGNN_GB_DU_MEM && RT == 1;
-  float du[DUM ? 1 : RT][16];
+  float du[RT][16];
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float dz[4], zu[4];
-      const float4 u4 = bld4_p<GGNN_GB_AUX>(pu, qm_vo(hh, n, H), qm_so(rt, q, H)), c4 = bld4_p<GGNN_GB_AUX>(pc, qm_vo(hh, n, H), qm_so(rt, q, H));
+      const float4 u4 = bld4_p<kGbAux>(pu, qm_vo(hh, n, H), qm_so(rt, q, H)), c4 = bld4_p<kGbAux>(pc, qm_vo(hh, n, H), qm_so(rt, q, H));
       const float uq[4] = {u4.x, u4.y, u4.z, u4.w}, cq[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld_p<GGNN_GB_AUX>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld_p<GGNN_GB_H_AUX>(ph, vo, so);
+        const float d = bld_p<kGbAux>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld_p<0>(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
-        if constexpr (DUM) bst(pdo, d * u, vo, so);
-        else du[rt][4 * q + i] = d * u;
+        du[rt][4 * q + i] = d * u;
         csum += dz[i];
         usum += zu[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, dz[i]);
@@ -328,19 +314,16 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float zr[4];
-      const float4 r4 = bld4_p<GGNN_GB_AUX>(pr, qm_vo(hh, n, H), qm_so(rt, q, H));
+      const float4 r4 = bld4_p<kGbAux>(pr, qm_vo(hh, n, H), qm_so(rt, q, H));
       const float rq[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * q + i;
         const int ro = rt * 32 + acc_row0(r);
         const int so = ro * H * 4;
-        const float h = bld_p<GGNN_GB_H_AUX>(ph, vo, so), rr = rq[i];
+        const float h = bld_p<0>(ph, vo, so), rr = rq[i];
         const float drh = a2[rt][r];
-        float dur;
-        if constexpr (DUM) dur = bld(pdo, vo, so);
-        else dur = du[rt][r];
-        a2[rt][r] = dur + drh * rr;
+        a2[rt][r] = du[rt][r] + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);
         rsum += zr[i];
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);

@@ -27,9 +27,9 @@
 #include "ggnn_common.h"
 
 #define PAIR_TILE 32   // rows per product tile (the ring kernel's 32-row variant)
-#ifndef PAIR_CHUNK
-#define PAIR_CHUNK 16  // tiles per split-K term list of the dW product (512 rows)
-#endif
+// tiles per split-K term list of the dW product (512 rows; 4 and 8 measured
+// slower: more chunks, more atomics)
+#define PAIR_CHUNK 16
 
 // S1: in-degree per (channel, node row) from the staged 16-bit rows (0/1
 // limbs: nonzero bits <=> 1); one block per (graph, channel) tile, a wave per row

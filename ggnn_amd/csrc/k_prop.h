@@ -7,17 +7,10 @@
 #pragma once
 #include "ggnn_common.h"
 
-// cache policy of the adjacency LDS-DMA: nontemporal (each tile is read once
-// per launch; measured -1.5 % on k_prop_bwd)
-#ifndef GGNN_PB_AUX
-#define GGNN_PB_AUX kNT  // k_prop_bwd's dh_in loads (read once; -0.9 %)
-#endif
-#ifndef GGNN_PB_DX_NT
-#define GGNN_PB_DX_NT 0  // nontemporal dX^T loads (experiment)
-#endif
-#ifndef GGNN_PROP_A_AUX
-#define GGNN_PROP_A_AUX kNT
-#endif
+// cache policies: the adjacency LDS-DMA is nontemporal (each tile is read
+// once per launch; measured -1.5 % on k_prop_bwd), and so are k_prop_bwd's
+// dh_in loads (read once; -0.9 %).  (Nontemporal dX^T loads measured no gain.)
+constexpr int kPropAAux = kNT, kPbAux = kNT;
 
 // ===========================================================================
 // k_prop_fwd: per channel c
@@ -65,9 +58,9 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 
   stage_rows_k<PREC, V, H, NT>(h_hi, h_lo, hs_in + rowg * H, H, tid);
   const u16* ag = Ab + (long)g * C * V * V;
-  if (nc > 0) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(0), ag + (long)chan(0) * V * V, tid);
+  if (nc > 0) glds_tile<ACH, V, NT, kPropAAux>(abuf_of(0), ag + (long)chan(0) * V * V, tid);
   __syncthreads();
-  if (NAB == 2 && nc > 1) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(1), ag + (long)chan(1) * V * V, tid);
+  if (NAB == 2 && nc > 1) glds_tile<ACH, V, NT, kPropAAux>(abuf_of(1), ag + (long)chan(1) * V * V, tid);
 
   f32x16 accx[VT];
 #pragma unroll
@@ -98,7 +91,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (SPLIT) b_pipeline<KS, 2>(ldw, mt);
     else b_direct<KS, KS>(ldw, mt);
     __syncthreads();  // S1: A_c visible (two tiles: and every wave is past AGG(c-1))
-    if (NAB == 2 && ci >= 1 && ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(ci + 1), ag + (long)chan(ci + 1) * V * V, tid);
+    if (NAB == 2 && ci >= 1 && ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf_of(ci + 1), ag + (long)chan(ci + 1) * V * V, tid);
     const char* abuf = abuf_of(ci);
     // ---- AGG: X[i][n] += sum_j A_c[i][j] M_c[j][n]
 #pragma unroll
@@ -116,7 +109,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
     if constexpr (NAB == 1) {
       __syncthreads();  // S2: A_c reads done
       // A_{c+1} lands in LDS by DMA while MT(c+1) runs (drained by its S1)
-      if (ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf_of(0), ag + (long)chan(ci + 1) * V * V, tid);
+      if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf_of(0), ag + (long)chan(ci + 1) * V * V, tid);
     }
   }
 
@@ -191,14 +184,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     const Act* p = dXT + wg_off(n, rowg + 16 * s + 8 * hh, H);  // K-blocked (ggnn_common.h)
     if constexpr (SPLIT) {
       typedef float f4v __attribute__((ext_vector_type(4)));
-      f4v a, b;
-      if (GGNN_PB_DX_NT) {
-        a = __builtin_nontemporal_load((const f4v*)p);
-        b = __builtin_nontemporal_load((const f4v*)(p + 4));
-      } else {
-        a = *(const f4v*)p;
-        b = *(const f4v*)(p + 4);
-      }
+      const f4v a = *(const f4v*)p, b = *(const f4v*)(p + 4);
       const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       dxh[s] = pk8<true>(x);
       dxl[s] = pk8_lo<true>(x);
@@ -213,14 +199,14 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   const int nc = cl[0];
   auto chan = [&](int i) { return cl[1 + i]; };
   const u16* ag = AbT + (long)g * C * V * V;
-  if (nc > 0) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf, ag + (long)chan(0) * V * V, tid);
+  if (nc > 0) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(0) * V * V, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
   const int vo = (4 * hh * H + n) * 4;
   f32x16 adh[VT];
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) adh[jt][r] = bld_p<GGNN_PB_AUX>(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
+    for (int r = 0; r < 16; ++r) adh[jt][r] = bld_p<kPbAux>(rdh, vo, (jt * 32 + acc_row0(r)) * H * 4);
   __syncthreads();
 
   for (int ci = 0; ci < nc; ++ci) {
@@ -266,7 +252,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     }
     __syncthreads();  // S1: dM images complete, A_c reads done
     // A_{c+1} lands in LDS by DMA while phase b runs (drained by S2)
-    if (ci + 1 < nc) glds_tile<ACH, V, NT, GGNN_PROP_A_AUX>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
+    if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
     auto ldb = [&](int ks) {

@@ -15,6 +15,13 @@ reduced gradient, so it runs after this reduction (optimizer, next row).
 
 ``torch.distributed`` with backend "nccl" is RCCL on ROCm; "gloo" is used by
 the CPU tests.
+
+A collective normally runs only when the group has more than one rank.  An
+explicit backend passed to ``init_from_env`` at WORLD_SIZE 1 (bench.py
+``--dist-backend nccl`` under a one-rank torchrun) still creates the process
+group and turns the collectives on (``collectives_at_world_one``), so the
+RCCL path that an N-GPU run takes can be executed on a one-GPU box: the sum
+over one rank leaves every value unchanged.
 """
 from __future__ import annotations
 
@@ -22,6 +29,25 @@ import os
 
 import torch
 import torch.distributed as tdist
+
+_ALWAYS = False   # collectives at world size 1 (init_from_env with an explicit backend)
+
+
+def collectives_at_world_one(on: bool | None = None) -> bool:
+    """Whether FlatGradients.all_reduce / all_reduce_sum issue their collective
+    in a one-rank group (set by init_from_env with an explicit backend at
+    WORLD_SIZE 1; ``on`` overrides).  Returns the setting."""
+    global _ALWAYS
+    if on is not None:
+        _ALWAYS = bool(on)
+    return _ALWAYS
+
+
+def _reducing(group) -> bool:
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return False
+    return tdist.get_world_size(group) > 1 or _ALWAYS
+
 
 GRAD_ORDER = ("edge_weights", "edge_biases", "gates_kernel", "gates_bias",
               "candidate_kernel", "candidate_bias")
@@ -66,7 +92,7 @@ class FlatGradients:
 
     def all_reduce(self, group=None) -> None:
         """Sum the gradients over all ranks (RCCL on GPUs, gloo on CPU)."""
-        if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size(group) > 1:
+        if _reducing(group):
             tdist.all_reduce(self.flat, op=tdist.ReduceOp.SUM, group=group)
 
 
@@ -108,19 +134,26 @@ class FlatTrainBuffer:
 
 def all_reduce_sum(group=None):
     """A callable summing a tensor over the ranks of `group` (RCCL on GPUs,
-    gloo on CPU), or None outside a multi-rank job."""
-    if not (tdist.is_available() and tdist.is_initialized() and tdist.get_world_size(group) > 1):
+    gloo on CPU), or None outside a multi-rank job (a one-rank group counts
+    as multi-rank when collectives_at_world_one() is on)."""
+    if not _reducing(group):
         return None
     return lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
 
 
 def init_from_env(backend: str | None = None):
     """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE,
-    LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local_rank)."""
+    LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local_rank).
+
+    backend None: a group only when WORLD_SIZE > 1 (nccl = RCCL on a GPU, else
+    gloo).  An explicit backend at WORLD_SIZE 1 also creates the (one-rank)
+    group, needs MASTER_ADDR / MASTER_PORT, and turns the collectives on
+    (collectives_at_world_one): the rehearsal of the N-rank RCCL path on one
+    GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not tdist.is_initialized():
+    if (world > 1 or backend is not None) and not tdist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -128,4 +161,6 @@ def init_from_env(backend: str | None = None):
             tdist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             tdist.init_process_group(backend)
+        if world == 1:
+            collectives_at_world_one(True)
     return rank, world, local

@@ -139,6 +139,28 @@ class CapturedStep:
         self.out = None
         self.runs = 0               # batches this step has run (eager first, then replays)
 
+    def nbytes(self) -> int:
+        """Device bytes this step holds: its input buffer, the engine's staged
+        adjacency and workspaces, the heads' workspace and the graph's outputs
+        (the activations the captured body allocates in the graph's private
+        pool are small beside the engine's training workspace)."""
+        n = self.inputs.buf.numel()
+        eng = self.engine
+        if getattr(eng, "_adj", None) is not None:
+            n += eng._adj.numel()
+        n += sum(w.numel() for w in getattr(eng, "_ws", {}).values())
+        ws = getattr(self.heads, "_ws", None)
+        if ws is not None:
+            n += ws.numel()
+        return int(n)
+
+    def release(self) -> None:
+        """Free the graph and every buffer it references (eviction)."""
+        if self.graph is not None:
+            self.graph.reset()
+        self.graph = self.out = None
+        self.engine = self.heads = self.inputs = None
+
 
 def edge_arrays(graphs, v: int, num_edge_types: int):
     """(edges int32 [n, 3], offsets int32 [b + 1]) of a batch's per-graph edge

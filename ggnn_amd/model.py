@@ -30,7 +30,9 @@ carry the autograd graph around the call.
 """
 from __future__ import annotations
 
+import random
 import time
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -150,6 +152,12 @@ class DenseGGNNChemModel(BtbBatching):
         self.ops = {}
         self._engines = {}
         self._up_labels, self._up_labels_e = Uploader(), Uploader()
+        # the reference seeds Python's and numpy's global RNGs here
+        # (chem_tensorflow.py:174-175): minibatch_schedule shuffles with the
+        # global numpy RNG, so ranks of a data-parallel job that construct their
+        # models alike run the same schedule (run_epoch checks that they do)
+        random.seed(self.params["random_seed"])
+        np.random.seed(self.params["random_seed"])
         rs = self.params["random_seed"] if seed is None else seed
         self._rng = np.random.RandomState(rs)
         self.prepare_specific_graph_model()
@@ -166,6 +174,7 @@ class DenseGGNNChemModel(BtbBatching):
             "edge_weight_dropout_keep_prob": 1,
             "compact_adjacency": False,   # not in the reference: edge-list feed (ggnn_set_adjacency_edges)
             "hip_graphs": True,           # not in the reference: captured steps for edge-list feeds (graphs.py)
+            "hip_graph_cache_mb": 6144,   # not in the reference: device memory the captured steps may hold
         }
 
     @property
@@ -210,11 +219,13 @@ class DenseGGNNChemModel(BtbBatching):
         self._front_end = None
         self._heads = None
         self._flat = None
-        self._graphs = {}           # hipGraph-captured steps by batch shape (graphs.py)
+        # hipGraph-captured steps by batch shape (graphs.py), least recently
+        # used first; bounded by params['hip_graph_cache_mb'] (_evict_graphs)
+        self._graphs = OrderedDict()
         self._ring = None
         # batches by path: captured-step replays, first batches of a shape
         # (eager, on the step's device inputs), the plain eager path
-        self.graph_stats = {"captured": 0, "replayed": 0, "uncaptured": 0, "eager": 0}
+        self.graph_stats = {"captured": 0, "replayed": 0, "uncaptured": 0, "eager": 0, "evicted": 0}
         self.lookup_sqnorm = {}
         self.optimizer = None
 
@@ -507,7 +518,8 @@ class DenseGGNNChemModel(BtbBatching):
         target_num = float(count + SMALL_NUMBER)
         keeps = (float(ph.get("emb_dropout_keep_prob", 1.0)),) + self._path_keeps() + (self._out_keep(),)
         adam = training and all_reduce is None
-        key = (bool(training), adam, b, v, wi.shape[-1], keeps, task_id)
+        # (grad_scale is baked into the captured Adam launch: part of the key)
+        key = (bool(training), adam, b, v, wi.shape[-1], keeps, task_id, float(grad_scale) if adam else 1.0)
         if training:
             fl = self.train_buffer()
             params = self.trainable_variables()
@@ -520,6 +532,7 @@ class DenseGGNNChemModel(BtbBatching):
             cs = CapturedStep(StepLayout(b, v, wi.shape[-1], o, oe), eng, OutputHeads(self.params["hidden_size"]),
                               self.device)
             self._graphs[key] = cs
+        self._graphs.move_to_end(key)
         seeds = [self._seed() for _ in range(3)]
         step = 0
         if adam:
@@ -545,7 +558,7 @@ class DenseGGNNChemModel(BtbBatching):
             if training:
                 probs = self._forward_backward(fl, params, None, task_id, sf)
                 if adam:
-                    self._apply_gradients(fl, params, 1.0, step_dev=inp.step)
+                    self._apply_gradients(fl, params, grad_scale, step_dev=inp.step)
                 loss = fl.loss.sum()
             else:
                 probs, loss = self._forward_eval(sf, task_id)
@@ -567,14 +580,39 @@ class DenseGGNNChemModel(BtbBatching):
             out = cs.out
             self.graph_stats["replayed"] += 1
         cs.runs += 1
+        if cs.runs == 1:
+            self._evict_graphs(keep=key)
         probs = out["probs"]
         self.ops["computed_values"] = probs[0].reshape(b, v * o)
         self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
-        self.ops["loss"] = out["loss"]
+        loss = out["loss"]
         if training and not adam:
             all_reduce(fl.flat)
             self._apply_gradients(fl, params, grad_scale)
-        return out["loss"]
+            # the union-batch loss: the graph's loss sum was taken before the
+            # all-reduce (this rank's share), the eager path's after it
+            loss = fl.loss.sum()
+        self.ops["loss"] = loss
+        return loss
+
+    def _evict_graphs(self, keep=None) -> None:
+        """Drop the least recently used captured steps (their graph, engine
+        workspaces, heads workspace and input buffer) while the cache holds
+        more than params['hip_graph_cache_mb'] of device memory.  Bucketed
+        treebanks have a full and a tail batch shape per bucket, for training
+        and evaluation; unbounded, their workspaces (~0.9 GB at hidden 400,
+        b = 20, v = 120) grew to tens of GB per process."""
+        budget = float(self.params.get("hip_graph_cache_mb", 6144)) * 2 ** 20
+        total = sum(cs.nbytes() for cs in self._graphs.values())
+        while total > budget and len(self._graphs) > 1:
+            k = next(iter(self._graphs))
+            if k == keep:
+                self._graphs.move_to_end(k)
+                k = next(iter(self._graphs))
+            cs = self._graphs.pop(k)
+            total -= cs.nbytes()
+            cs.release()
+            self.graph_stats["evicted"] += 1
 
     def _forward_eval(self, sf, task_id=0):
         """build_loss's forward without autograd on a _StepFeed: front-end ->
@@ -804,6 +842,27 @@ class DenseGGNNChemModel(BtbBatching):
         # keeps the probabilities in its returned lists)
         return float(hl.sum()), self._score_arrays(p["ph"], hp.numpy().copy(), hpe.numpy().copy())
 
+    def _check_schedule_agrees(self, sched) -> None:
+        """Data parallel: every rank must draw the same epoch schedule (the
+        rank-sharded iterator assumes it; the shuffles use the global numpy
+        RNG, seeded by the constructor as chem_tensorflow.py:174-175 does).
+        One collective per epoch compares a 62-bit digest of (bucket, sentence
+        ids) of every batch across the ranks; a mismatch raises instead of
+        silently training some batches twice and others never."""
+        import hashlib
+        hsh = hashlib.blake2b(digest_size=8)
+        for bidx, els in sched:
+            hsh.update(repr((bidx, [d.get("id") for d in els])).encode())
+        dg = int.from_bytes(hsh.digest(), "little") >> 2
+        dev = self.device if torch.distributed.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([dg, -dg], dtype=torch.int64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=self.group)
+        hi, lo = int(t[0].item()), -int(t[1].item())
+        if hi != lo:
+            raise RuntimeError("rank %d: the ranks drew different minibatch schedules (digest %d, range [%d, %d]); "
+                               "seed np.random identically on every rank (params['random_seed'])"
+                               % (self.rank, dg, lo, hi))
+
     # the reference's per-task "chemical accuracy" normalisers (chem_tensorflow.py:529-531)
     CHEMICAL_ACCURACIES = np.array([0.066513725, 0.012235489, 0.071939046, 0.033730778, 0.033486113, 0.004278493,
                                     0.001330901, 0.004165489, 0.004128926, 0.00409976, 0.004527465, 0.012292586,
@@ -866,7 +925,10 @@ class DenseGGNNChemModel(BtbBatching):
         all_reduce = _dist.all_reduce_sum(self.group) if world > 1 else None
         if world > 1 and all_reduce is None:
             raise RuntimeError("world_size %d but torch.distributed is not initialised" % world)
-        it = self.make_minibatch_iterator(data, is_training, rank=self.rank, world_size=world)
+        sched = self.minibatch_schedule(data, is_training)
+        if world > 1:
+            self._check_schedule_agrees(sched)
+        it = self.make_minibatch_iterator(data, is_training, rank=self.rank, world_size=world, schedule=sched)
         for feed in ThreadedIterator(it, max_queue_size=5):
             if int(feed["num_graphs"]) == 0:     # no batch for this rank in the last global step
                 if is_training:

@@ -211,3 +211,90 @@ def test_flat_train_buffer_layout():
     assert float(fb.flat.sum()) == 7.0 + 8.0 + 6.0
     fb.zero_()
     assert float(fb.flat.abs().sum()) == 0.0
+
+
+def _world_one_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as tdist
+    from ggnn_amd.dist import FlatGradients, FlatTrainBuffer, all_reduce_sum, collectives_at_world_one, init_from_env
+    r, w, _ = init_from_env(backend="gloo")      # explicit backend at WORLD_SIZE 1: a one-rank group
+    ok = [tdist.is_initialized(), tdist.get_world_size() == 1, collectives_at_world_one()]
+    fg = FlatGradients(8, 4, True)
+    fg.flat.copy_(torch.arange(fg.flat.numel(), dtype=torch.float32) * 0.5)
+    ref = fg.flat.clone()
+    fg.all_reduce()
+    fb = FlatTrainBuffer([torch.zeros(3, 5), torch.zeros(7)], n_sq=4, n_loss=2)
+    fb.flat.normal_()
+    ref2 = fb.flat.clone()
+    ar = all_reduce_sum()
+    ok += [ar is not None, torch.equal(fg.flat, ref)]
+    ar(fb.flat)
+    ok.append(torch.equal(fb.flat, ref2))
+    tdist.barrier()
+    tdist.destroy_process_group()
+    q.put(ok)
+
+
+def test_explicit_backend_at_world_one_runs_the_collectives():
+    """init_from_env with an explicit backend at WORLD_SIZE 1 (bench.py
+    --dist-backend nccl under a one-rank torchrun) creates the one-rank group
+    and FlatGradients.all_reduce / all_reduce_sum issue their collective; the
+    sum over one rank leaves every value unchanged (the GPU test runs the same
+    calls over RCCL)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world_one_worker, args=(_free_port(), q))
+    p.start()
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert q.get(timeout=5) == [True] * 6
+
+
+def _schedule_worker(rank, world, port, diverge, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as tdist
+    from ggnn_amd.dist import init_from_env
+    init_from_env(backend="gloo")
+    m, data = _golden_model()
+    m.rank, m.world_size = rank, world
+    if diverge and rank == 1:
+        np.random.seed(123)
+    sched = m.minibatch_schedule(m.process_raw_graphs(data, True), True)
+    try:
+        m._check_schedule_agrees(sched)
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, "raised" if "different minibatch schedules" in str(e) else repr(e)))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("diverge", [False, True])
+def test_ranks_check_that_their_schedules_agree(diverge):
+    """The model seeds the global RNGs as the reference does
+    (chem_tensorflow.py:174-175), so ranks draw the same schedule; run_epoch
+    compares a digest of it across the ranks once per epoch and raises when a
+    rank's shuffles differ (one collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_schedule_worker, args=(r, 2, port, diverge, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get(timeout=5) for _ in range(2))
+    assert got == {0: "raised", 1: "raised"} if diverge else got == {0: "ok", 1: "ok"}, got
+
+
+def test_model_seeds_the_global_rngs_like_the_reference():
+    import random
+    np.random.seed(99)
+    random.seed(99)
+    _golden_model()                   # params random_seed = 0 (chem_tensorflow.py:174-175)
+    a, b = np.random.rand(), random.random()
+    np.random.seed(0)
+    random.seed(0)
+    assert (a, b) == (np.random.rand(), random.random())

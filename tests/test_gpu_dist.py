@@ -132,3 +132,63 @@ def test_bench_two_ranks_rehearsal():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["scaling"] == "weak" and res["config"]["global_batch"] == 512
     assert res["value"] > 0 and "cpu_baseline" not in res
+
+
+def test_two_rank_captured_step_returns_the_union_loss(tmp_path):
+    """Edge-list feeds with hipGraph-captured steps at world size 2: the
+    captured step's loss is summed inside the graph BEFORE the all-reduce,
+    so the returned loss must be re-summed after it (the union-batch loss,
+    chem_tensorflow.py:358-360,399-403), exactly as the eager path returns
+    it; weights equal after three steps (the first batch of the shape runs
+    its body eagerly, the second is captured, the third replays)."""
+    out = str(tmp_path / "graph_loss.npz")
+    _spawn("dist_graph_loss_worker.py", [out], tmp_path)
+    d = np.load(out)
+    assert int(d["uncaptured"]) == 1 and int(d["replayed"]) == 2 and int(d["eager_steps"]) == 3
+    np.testing.assert_allclose(d["graph_loss"], d["eager_loss"], rtol=1e-5)
+    assert float(d["param_diff"]) <= 1e-5 * max(float(d["param_scale"]), 1.0)
+
+
+def test_rccl_one_rank_group_runs_the_training_collectives(tmp_path):
+    """The RCCL path an N-GPU run takes, executed on the test box's one GPU: a
+    one-rank "nccl" group made exactly as dist.init_from_env makes it
+    (device_id=), the per-step all-reduce of FlatGradients (bench.py's step)
+    and of FlatTrainBuffer (train_step, eager and hipGraph-captured) issued
+    through the same calls, values unchanged by the one-rank sum, then
+    barrier and destroy."""
+    out = str(tmp_path / "rccl.json")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist_rccl_worker.py"), out], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    with open(out) as f:
+        res = json.load(f)
+    print("rccl one-rank:", res)
+    assert res["backend"] == "nccl" and res["world"] == 1 and res["always"]
+    assert res["flat_gradients_unchanged"] and res["all_reduce_sum_callable"]
+    for tag in ("eager", "captured"):
+        assert res[tag + "_train_buffer_unchanged"], tag
+        la, l1 = res[tag + "_losses"]
+        np.testing.assert_allclose(la, l1, rtol=1e-6)
+        # (the two models' backward atomics sum in different orders)
+        assert res[tag + "_param_max_diff"] <= 1e-5 * max(res[tag + "_param_scale"], 1.0), (tag, res)
+    assert res["captured_graph_stats"]["replayed"] == 2
+    assert res["destroyed"]
+
+
+def test_bench_one_rank_rccl_rehearsal():
+    """bench.py under a one-rank torchrun with --dist-backend nccl: the
+    one-rank RCCL group is created, the per-step all-reduce runs inside the
+    timed loop, and the JSON line names the backend."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "1", "--steps", "3",
+           "--warmup", "1", "--no-side", "--no-cpu-baseline", "--dist-backend", "nccl"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 1 and res["value"] > 0
+    assert res["all_reduce"]["backend"] == "nccl" and res["all_reduce"]["bytes_per_step"] > 0

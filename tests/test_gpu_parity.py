@@ -239,6 +239,45 @@ def test_full_config3_backward_at_loss_scale():
         assert _nmax(full[k], h1[k] + h2[k]) <= 1e-5, k
 
 
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("dropout", [False, True])
+def test_full_config3_all_gradients_vs_float64_oracle(dropout):
+    """The bench's own workload, configs[2] at full size (b = 256, v = 128,
+    h = 256, C = 8, T = 5): h_T and ALL SEVEN gradients of the whole batch
+    against the float64 oracle run over the whole batch -- the weight
+    gradients sum 256 x 128 x 5 rows of single-f16-operand products with fp32
+    atomics (k_wgrad256), which the per-graph checks above do not reach.
+    dropout=False: once with N(0,1) dL/dh_T and once with the same dL/dh_T
+    at the btb loss's scale 2^-14 (a power of two, so the oracle's gradients
+    scale exactly; the engine picks another backward gscale).  dropout=True:
+    the reference's training feed, keep 0.9 for edge weights and GRU state
+    (chem_tensorflow_dense.py:860-861), the same Philox seed on both sides.
+    Bar: max |err| / max |ref| <= 1e-3 (FP32_TOL), per gradient.
+    References: chem_tensorflow.py:496; chem_tensorflow_dense.py:391-437."""
+    b, v, h, C, T = 256, 128, 256, 8, 5
+    A, h0, w = _case(b, v, h, C, seed=4)
+    dhT = np.random.default_rng(14).standard_normal((b, v, h)).astype(np.float32)
+    A64, w64 = A.astype(np.float64), _f64(w)
+    dr = dict(edge_keep=0.9, state_keep=0.9, seed=0x5EED_0004) if dropout else None
+    ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
+    gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
+    del caches
+    errs = {}
+    for scale in ((1.0,) if dropout else (1.0, 2.0 ** -14)):
+        d = (dhT * np.float32(scale)).astype(np.float32)
+        got = _run_dropout(A, h0, w, T, "fp32", dr, d) if dropout else _run(A, h0, w, T, "fp32", dhT=d)
+        e = {"hT": float(np.abs(got["hT"] - ref).max())}
+        for k in GRADS:
+            e[k] = _nmax(got[k].reshape(gref[k].shape), scale * gref[k])
+        errs[scale] = e
+        del got
+    print("config 3 full batch, dropout=%s:" % dropout, errs)
+    for scale, e in errs.items():
+        assert e["hT"] <= FP32_TOL, (scale, e)
+        for k in GRADS:
+            assert e[k] <= FP32_TOL, (scale, k, e)
+
+
 @pytest.mark.parametrize("b,v,h,C,T", SHAPES)
 def test_forward_bf16_matches_rounding_emulation(b, v, h, C, T):
     A, h0, w = _case(b, v, h, C, seed=b * 7 + v)
