@@ -198,7 +198,7 @@ PackL pack_layout(const Cfg& c) {
 
 // ---- staged adjacency
 struct AdjL {
-  size_t Ab, AbT, deg, chl, chl_all, total;
+  size_t Ab, AbT, deg, chl, chl_all, occ, cgl, total;
 };
 AdjL adj_layout(const Cfg& c) {
   AdjL L;
@@ -208,6 +208,8 @@ AdjL adj_layout(const Cfg& c) {
   L.deg = o; o += al((size_t)c.b * c.C * c.V * 2);
   L.chl = o; o += al((size_t)c.b * (c.C + 1) * 4);  // per-graph non-empty channel lists (k_chan_list)
   L.chl_all = o; o += al((size_t)(c.C + 1) * 4);     // identity list (dense channel loop)
+  L.occ = o; o += al((size_t)c.b * c.C);              // (graph, channel) occupancy bytes
+  L.cgl = o; o += al((size_t)c.C * (c.b + 1) * 4);    // per-channel graph lists (k_chan_graphs)
   L.total = o;
   return L;
 }
@@ -314,6 +316,25 @@ void launch_prop_fwd(const Cfg& c, int t, const void* hs, const u16* Ab, ChanL c
   hipLaunchKernelGGL((k_prop_fwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)hs, Ab, chl.p, chl.stride,
                      P<u16>(pk, PL.wf(c.ed ? t : 0)), PL.loW, P<float>(pk, PL.beta), (ActT<PREC>*)Xa, (u16*)XT, c.C, c.N);
 }
+// k_wgrad256's K chunk at hidden 256 (one workgroup per CU, 128 KiB LDS
+// ring): the largest chunk that still gives >= 7/8 of the CUs a tile-chunk;
+// the problems hold 6 + C tiles of 256 x 256 (dWg 4, dWc 2, dW one per channel)
+long wg256_kc(const Cfg& c) {
+  const long N = c.N, tiles_eq = 6 + c.C;
+  long KC = 8192;
+  while (KC > 128 && ((N % KC) != 0 || tiles_eq * (N / KC) < 224)) KC /= 2;
+  return KC;
+}
+// whether dW_c runs over channel c's graph list (k_chan_graphs) instead of
+// every row: the specialised path at hidden 256 with channel skipping, when a
+// K chunk's share of the graphs fits the kernel's register list.  Then
+// k_prop_bwd writes no dM^T rows for a graph's empty channels.
+bool wgrad_lists(const Cfg& c) {
+  if (!(c.H == 256 && c.N % 128 == 0) || (c.flags & GGNN_DENSE_CHANNELS)) return false;
+  const long KC = wg256_kc(c), nchunks = c.N / KC;
+  return (c.b + nchunks - 1) / nchunks <= WG_LIST_MAX && c.V % 32 == 0;
+}
+
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, ChanL chl,
                      const PackL& PL, const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp,
@@ -322,7 +343,7 @@ void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg, chl.p,
                      chl.stride,
                      P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1,
-                     gmax);
+                     gmax, (int)!wgrad_lists(c));
 }
 template <int H, int RT, int PREC>
 void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const float* hf, const PackL& PL,
@@ -582,7 +603,7 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   // all weight gradients in one grouped launch over every timestep (measured:
   // 20 % faster than one launch per timestep right after its producers, whose
   // operands would still sit in the Infinity Cache)
-  if (int e = wgrad_impl<PREC>(c, ws, 0, c.T, dW, dWg, dWc, s)) return e;
+  if (int e = wgrad_impl<PREC>(c, adj, ws, 0, c.T, dW, dWg, dWc, s)) return e;
   if (c.ed) {
     Prof p(K_WGRAD, s);
     hipLaunchKernelGGL(k_edge_mask_reduce, dim3(grid1d((long)c.C * H * H / 4)), dim3(256), 0, s,
@@ -617,7 +638,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
 // Weight gradients of timesteps [t0, t0 + nt): out[m][n] += sum_{t,rows}
 // P_t[m][row] Q_t[n][row], one grouped launch (k_wgrad.h).
 template <int PREC>
-int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, float* dWc, hipStream_t s) {
+int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* dW, float* dWg, float* dWc,
+               hipStream_t s) {
   const WsL L = ws_layout(c, true);
   const long N = c.N, H = c.H;
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
@@ -667,13 +689,19 @@ int wgrad_impl(const Cfg& c, void* ws, int t0, int nt, float* dW, float* dWg, fl
   // time (measured +0.27 ms per step at config 3 with keep 0.9)
   const long tiles_eq = c.ed ? tiles - (long)(nt - 1) * c.C * a.p[np - 1].tiles_b : tiles;
   if (big) {
-    // one workgroup per CU (128 KiB LDS ring): the largest K chunk that still
-    // gives >= 7/8 of the CUs a tile-chunk
-    int KC = 8192;
-    while (KC > 128 && ((N % KC) != 0 || tiles_eq * (N / KC) < 224)) KC /= 2;
+    const long KC = wg256_kc(c);
     if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
-    a.KC = KC;
+    if (tiles_eq != 6 + c.C) return fail(GGNN_EINVAL, "k_wgrad256: unexpected problem set");
+    a.KC = (int)KC;
     a.nchunks = (int)(N / KC);
+    if (wgrad_lists(c)) {
+      // dW_c over the rows of channel c's graphs only (the last problem)
+      WgProb& q = a.p[np - 1];
+      q.gl = P<const int>(adj, adj_layout(c).cgl);
+      q.gls = c.b + 1;
+      q.glmod = c.C;
+      q.V32 = c.V / 32;
+    }
     Prof p(K_WGRAD, s);
     hipLaunchKernelGGL((k_wgrad256<WP>), dim3(tiles * a.nchunks), dim3(512), 0, s, a);
     return GGNN_OK;
@@ -949,7 +977,9 @@ int ggnn_set_adjacency_edges(const ggnn_dims* d, void* adj, const int32_t* edges
     hipLaunchKernelGGL((k_adj_deg<VV, F>), dim3((unsigned)tiles), dim3(VV), 0, s, P<const u16>(adj, L.Ab),        \
                        P<u16>(adj, L.deg));                                                                      \
     hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,               \
-                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                              \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all), P<unsigned char>(adj, L.occ));                \
+    hipLaunchKernelGGL(k_chan_graphs, dim3(c.C), dim3(64), 0, s, P<const unsigned char>(adj, L.occ), c.b, c.C,   \
+                       P<int>(adj, L.cgl));                                                                      \
   } while (0)
   const bool f16 = c.prec != PREC_BF16;
   if (c.V == 32) { if (f16) ADJ_EDGES(32, true); else ADJ_EDGES(32, false); }
@@ -980,7 +1010,9 @@ int ggnn_set_adjacency(const ggnn_dims* d, void* adj, const float* A, ggnn_strea
     hipLaunchKernelGGL((k_prep_adj<VV, F>), grid, dim3(256), 0, s, A, c.vin, P<u16>(adj, L.Ab),                 \
                        P<u16>(adj, L.AbT), P<u16>(adj, L.deg));                                               \
     hipLaunchKernelGGL(k_chan_list<VV>, dim3(c.b), dim3(256), 0, s, P<const u16>(adj, L.deg), c.C,             \
-                       P<int>(adj, L.chl), P<int>(adj, L.chl_all));                                           \
+                       P<int>(adj, L.chl), P<int>(adj, L.chl_all), P<unsigned char>(adj, L.occ));              \
+    hipLaunchKernelGGL(k_chan_graphs, dim3(c.C), dim3(64), 0, s, P<const unsigned char>(adj, L.occ), c.b, c.C, \
+                       P<int>(adj, L.cgl));                                                                    \
   } while (0)
   if (c.prec != PREC_BF16) {
     if (c.V == 32) PREP_ADJ(32, true);

@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(V) k_adj_deg(const u16* __restrict__ Ab, u16* 
 // dense channel loop, GGNN_DENSE_CHANNELS: read with graph stride 0).
 template <int V>
 __global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, int C, int* __restrict__ chl,
-                                                   int* __restrict__ chl_all) {
+                                                   int* __restrict__ chl_all, unsigned char* __restrict__ occ) {
   __shared__ unsigned char fl[CHL_MAXC];
   const int g = blockIdx.x;
   if (g == 0) {
@@ -394,6 +394,7 @@ __global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, 
       any |= x.x | x.y | x.z | x.w;
     }
     fl[c] = any != 0;
+    occ[(long)g * C + c] = any != 0;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -403,6 +404,26 @@ __global__ void __launch_bounds__(256) k_chan_list(const u16* __restrict__ deg, 
       if (fl[c]) out[1 + n++] = c;
     out[0] = n;
   }
+}
+
+// per-channel graph lists cgl[c] = [count, graphs with an edge in channel c
+// (ascending)] from the (graph, channel) occupancy k_chan_list writes: the
+// weight-gradient kernel sums dW_c over those graphs' rows only.  One wave per
+// channel, 64 graphs per ballot.
+__global__ void __launch_bounds__(64) k_chan_graphs(const unsigned char* __restrict__ occ, int b, int C,
+                                                    int* __restrict__ cgl) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1;
+  int* o = cgl + (long)c * (b + 1);
+  int n = 0;
+  for (int g0 = 0; g0 < b; g0 += 64) {
+    const int g = g0 + lane;
+    const bool f = g < b && occ[(long)g * C + c];
+    const unsigned long long m = __ballot(f);
+    if (f) o[1 + n + __popcll(m & below)] = g;
+    n += __popcll(m);
+  }
+  if (lane == 0) o[0] = n;
 }
 
 // ---- all weight packs of one ggnn_pack_weights call in ONE launch: a job

@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
            const int* __restrict__ chl, int chs, const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
            u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
-           const uint32_t* __restrict__ gmax) {
+           const uint32_t* __restrict__ gmax, int zdm) {
   dr = drop_resolve(dr);  // (a device-resident key: loaded once)
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
@@ -314,16 +314,17 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       bst(rdo, x, vo, (jt * 32 + acc_row0(r)) * H * 4);
     }
   }
-  // empty channels: dM_c = A_c^T dX = 0 exactly.  Their dM^T rows (the graph's
-  // V*H contiguous elements of channel c, wg_off layout) and dbeta partials
-  // are written as zeros for the weight-gradient kernels.
+  // empty channels: dM_c = A_c^T dX = 0 exactly.  Their dbeta partials are
+  // written as zeros, and so are their dM^T rows (the graph's V*H contiguous
+  // elements of channel c, wg_off layout) when the weight-gradient kernel
+  // reads every row (zdm; with per-channel graph lists it skips them)
   if (nc < C) {
     for (int c = 0, p = 0; c < C; ++c) {
       if (p < nc && cl[1 + p] == c) {
         ++p;
         continue;
       }
-      if (dMT) {
+      if (dMT && zdm) {
         u16* z = dMT + (long)c * H * N + rowg * H;
         for (int q = tid; q < V * H / 8; q += NT) st16(z + q * 8, make_uint4(0, 0, 0, 0));
       }

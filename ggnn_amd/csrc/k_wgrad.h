@@ -20,7 +20,14 @@ struct WgProb {
   long sPb;                     // batch stride of P, applied to (batch index / pdiv)
   int pdiv, T;                  // T: timesteps summed by this problem
   int ldO, M, N, tiles_n, tiles_b, tile_begin;
+  // k_wgrad256 only: K runs over the rows of listed graphs instead of every row
+  // (dW_c over the graphs with an edge in channel c: the others' dM_c rows are
+  // zero and are not written).  List of batch index bi at gl + (bi % glmod) *
+  // gls: [count, graph, ...]; a graph is V32 slices of 32 rows.  nullptr: all rows.
+  const int* gl;
+  int gls, glmod, V32;
 };
+#define WG_LIST_MAX 256  // graphs of one K chunk held in registers (4 VGPRs)
 #define WG_MAXP 8
 struct WgArgs {
   WgProb p[WG_MAXP];
@@ -187,15 +194,37 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   // image: row r = 64 B, chunk slot pc holds logical chunk pc ^ ((r >> 2) & 3)
   auto soff = [](int row, int ch) { return row * BK * 2 + ((ch ^ ((row >> 2) & 3)) << 4); };
 
-  const int kits = args.KC / BK, nit = kits * pr.T;  // host guarantees nit % NBUF == 0
-  const long kbase = (long)chunk * args.KC;
   const u16* Pb = (const u16*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
   const u16* Qb = (const u16*)pr.Q + (long)bi * pr.sQb;
   float* const outp = pr.out + (long)bi * pr.sOb;
+  // K slices: the chunk's KC rows (kits slices) x T timesteps, or, with a graph
+  // list, the chunk's share of the listed graphs' slices (any count: nit may
+  // be 0 -- nothing to add -- and need not be a multiple of NBUF)
+  int kits = args.KC / BK;
+  long kbase = (long)chunk * args.KC;
+  int glr[4] = {0, 0, 0, 0};  // the chunk's graphs, lane-distributed (read back by readlane)
+  if (pr.gl) {
+    const int* list = pr.gl + (long)(bi % pr.glmod) * pr.gls;
+    const int cnt = list[0], per = (cnt + args.nchunks - 1) / args.nchunks;
+    const int gb = min(cnt, chunk * per), ge = min(cnt, gb + per);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glr[j] = (gb + j * 64 + lane < ge) ? list[1 + gb + j * 64 + lane] : 0;
+    kits = (ge - gb) * pr.V32;
+    kbase = 0;
+  }
+  const int nit = kits * pr.T;
+  if (nit == 0) return;
+  // row of slice `it`'s first K element: graph glr[i] (i = slice / V32) row (slice % V32) * 32
+  auto krow = [&](int sl) -> long {
+    if (!pr.gl) return kbase + (long)sl * BK;
+    const int i = sl / pr.V32;
+    const int v = i < 64 ? glr[0] : i < 128 ? glr[1] : i < 192 ? glr[2] : glr[3];
+    return (long)__builtin_amdgcn_readlane(v, i & 63) * (pr.V32 * 32) + (long)(sl % pr.V32) * 32;
+  };
 
   auto stage = [&](int it, char* bp, char* bq) {
     const int t = it / kits;
-    const long k0 = kbase + (long)(it % kits) * BK;
+    const long k0 = krow(it % kits);
     // wg_off layout at H = 256: the slice is one contiguous [256][32] block of
     // the (m0 / 256)-th [H][N] array
     const u16* P = Pb + (long)t * pr.stepP + (long)(m0 >> 8) * 256 * pr.ldP + (k0 >> 5) * 8192;
@@ -216,11 +245,13 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
 
   // prologue: slices 0, 1, 2 in flight
 #pragma unroll
-  for (int u = 0; u < NBUF - 1; ++u) stage(u, pslot(u), qslot(u));
+  for (int u = 0; u < NBUF - 1; ++u)
+    if (u < nit) stage(u, pslot(u), qslot(u));
   for (int it0 = 0; it0 < nit; it0 += NBUF) {
 #pragma unroll
     for (int u = 0; u < NBUF; ++u) {
       const int it = it0 + u;
+      if (it >= nit) break;
       // slice `it` landed (this wave's DMAs: the two younger slices may stay in flight)
       if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory");
       else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");

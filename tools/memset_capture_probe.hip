@@ -40,6 +40,23 @@ __global__ void k_readback(const unsigned char* p, unsigned char* out, size_t n)
     out[i] = p[i];
 }
 
+// part 2 kernels: X[i] = ctr + 1 (this launch's stamp); count Y[i] != want;
+// then advance ctr (one vector atomic, its own node: ordered after k_check)
+__global__ void k_stamp(unsigned* X, size_t n, const unsigned* ctr) {
+  const unsigned v = *ctr + 1;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) X[i] = v;
+}
+__global__ void k_check(const unsigned* Y, size_t n, const unsigned* ctr, int copy, unsigned* err) {
+  const unsigned want = copy ? *ctr + 1 : 0u;
+  unsigned bad = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    bad += Y[i] != want;
+  if (bad) atomicAdd(err, bad);
+}
+__global__ void k_bump(unsigned* ctr) {
+  if (threadIdx.x == 0) atomicAdd(ctr, 1u);
+}
+
 static const char* type_name(hipGraphNodeType t) {
   switch (t) {
     case hipGraphNodeTypeKernel: return "kernel";
@@ -140,6 +157,50 @@ int main() {
     CHK(hipGraphDestroy(g));
   }
   std::printf("memset_capture_probe: %d of %zu cases wrong\n", bad_cases, cases.size());
+
+  // Part 2: back-to-back replays without a host sync, as run_epoch issues them.
+  //   k_stamp: ctr += 1; X[i] = ctr          (every element)
+  //   memset(Y, 0) / memcpy(Y <- X)          (the node under test, 64 MiB)
+  //   k_check: counts i with Y[i] != expected (0, or ctr + 1 for the copy); k_bump: ctr += 1
+  // 200 launches of each graph in a row; any node overlapping its predecessor
+  // (inside one launch or across launches) shows up as mismatches.
+  {
+    const size_t n = (64u << 20) / 4;
+    unsigned *X, *Y, *ctr, *err;
+    CHK(hipMalloc(&X, n * 4));
+    CHK(hipMalloc(&Y, n * 4));
+    CHK(hipMalloc(&ctr, 4));
+    CHK(hipMalloc(&err, 4));
+    for (int kind = 0; kind < 2; ++kind) {
+      CHK(hipMemsetAsync(ctr, 0, 4, s));
+      CHK(hipMemsetAsync(err, 0, 4, s));
+      CHK(hipStreamSynchronize(s));
+      hipGraph_t g;
+      CHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      hipLaunchKernelGGL(k_stamp, dim3(2048), dim3(256), 0, s, X, n, ctr);
+      if (kind == 0) CHK(hipMemsetAsync(Y, 0, n * 4, s));
+      else CHK(hipMemcpyAsync(Y, X, n * 4, hipMemcpyDeviceToDevice, s));
+      hipLaunchKernelGGL(k_check, dim3(2048), dim3(256), 0, s, Y, n, ctr, kind, err);
+      hipLaunchKernelGGL(k_bump, dim3(1), dim3(64), 0, s, ctr);
+      CHK(hipStreamEndCapture(s, &g));
+      hipGraphExec_t ge;
+      CHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      const int reps = 200;
+      for (int r = 0; r < reps; ++r) CHK(hipGraphLaunch(ge, s));
+      CHK(hipStreamSynchronize(s));
+      unsigned herr = 0, hctr = 0;
+      CHK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+      CHK(hipMemcpy(&hctr, ctr, 4, hipMemcpyDeviceToHost));
+      std::printf("back-to-back %s node, 64 MiB, %d launches: counter %u, mismatching elements %u -> %s\n",
+                  kind ? "memcpy D2D" : "memset", reps, hctr, herr, (herr || hctr != (unsigned)reps) ? "BAD" : "ok");
+      CHK(hipGraphExecDestroy(ge));
+      CHK(hipGraphDestroy(g));
+    }
+    CHK(hipFree(X));
+    CHK(hipFree(Y));
+    CHK(hipFree(ctr));
+    CHK(hipFree(err));
+  }
   CHK(hipFree(buf));
   CHK(hipFree(out));
   CHK(hipStreamDestroy(s));
