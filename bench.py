@@ -499,6 +499,13 @@ def end_to_end_side(dev, rank=0, world=1, epochs=1, restrict=True):
                               "valid_batches_by_path": {k: s2[k] - s1[k] for k in s1}})
     res.update({k: res["epochs"][-1][k] for k in ("train_instances_per_sec", "valid_instances_per_sec",
                                                    "valid_las", "valid_uas")})
+    import torch
+    res["device_memory"] = {"peak_reserved_gb": torch.cuda.max_memory_reserved(dev) / 2 ** 30,
+                            "peak_allocated_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
+                            "captured_steps": len(m._graphs), "captured_steps_gb": m.graph_stats["cache_bytes"] / 2 ** 30,
+                            "cache_budget_gb": m.params["hip_graph_cache_mb"] / 1024,
+                            "note": "peak over the warm-up and timed epochs of the captured-step model (process "
+                                    "totals: the bench's earlier lines included)"}
     # the same epochs on the eager path (every library call launched from the
     # host): the graphs' gain, and the launches per batch they replace
     me = fresh(graphs=False)

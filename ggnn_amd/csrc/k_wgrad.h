@@ -203,20 +203,28 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   int kits = args.KC / BK;
   long kbase = (long)chunk * args.KC;
   int glr[4] = {0, 0, 0, 0};  // the chunk's graphs, lane-distributed (read back by readlane)
+  bool listed = false;        // K walks the list (else the contiguous rows from kbase)
   if (pr.gl) {
     const int* list = pr.gl + (long)(bi % pr.glmod) * pr.gls;
     const int cnt = list[0], per = (cnt + args.nchunks - 1) / args.nchunks;
     const int gb = min(cnt, chunk * per), ge = min(cnt, gb + per);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) glr[j] = (gb + j * 64 + lane < ge) ? list[1 + gb + j * 64 + lane] : 0;
     kits = (ge - gb) * pr.V32;
-    kbase = 0;
+    if (ge > gb) {
+      const int g0 = list[1 + gb], g1 = list[ge];
+      if (g1 - g0 == ge - gb - 1) {
+        kbase = (long)g0 * pr.V32 * 32;  // consecutive graphs: their rows are contiguous
+      } else {
+        listed = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glr[j] = (gb + j * 64 + lane < ge) ? list[1 + gb + j * 64 + lane] : 0;
+      }
+    }
   }
   const int nit = kits * pr.T;
   if (nit == 0) return;
   // row of slice `it`'s first K element: graph glr[i] (i = slice / V32) row (slice % V32) * 32
   auto krow = [&](int sl) -> long {
-    if (!pr.gl) return kbase + (long)sl * BK;
+    if (!listed) return kbase + (long)sl * BK;
     const int i = sl / pr.V32;
     const int v = i < 64 ? glr[0] : i < 128 ? glr[1] : i < 192 ? glr[2] : glr[3];
     return (long)__builtin_amdgcn_readlane(v, i & 63) * (pr.V32 * 32) + (long)(sl % pr.V32) * 32;

@@ -174,7 +174,7 @@ class DenseGGNNChemModel(BtbBatching):
             "edge_weight_dropout_keep_prob": 1,
             "compact_adjacency": False,   # not in the reference: edge-list feed (ggnn_set_adjacency_edges)
             "hip_graphs": True,           # not in the reference: captured steps for edge-list feeds (graphs.py)
-            "hip_graph_cache_mb": 6144,   # not in the reference: device memory the captured steps may hold
+            "hip_graph_cache_mb": 16384,  # not in the reference: device memory the captured steps may hold
         }
 
     @property
@@ -225,7 +225,7 @@ class DenseGGNNChemModel(BtbBatching):
         self._ring = None
         # batches by path: captured-step replays, first batches of a shape
         # (eager, on the step's device inputs), the plain eager path
-        self.graph_stats = {"captured": 0, "replayed": 0, "uncaptured": 0, "eager": 0, "evicted": 0}
+        self.graph_stats = {"captured": 0, "replayed": 0, "uncaptured": 0, "eager": 0, "evicted": 0, "cache_bytes": 0}
         self.lookup_sqnorm = {}
         self.optimizer = None
 
@@ -602,7 +602,7 @@ class DenseGGNNChemModel(BtbBatching):
         treebanks have a full and a tail batch shape per bucket, for training
         and evaluation; unbounded, their workspaces (~0.9 GB at hidden 400,
         b = 20, v = 120) grew to tens of GB per process."""
-        budget = float(self.params.get("hip_graph_cache_mb", 6144)) * 2 ** 20
+        budget = float(self.params.get("hip_graph_cache_mb", 16384)) * 2 ** 20
         total = sum(cs.nbytes() for cs in self._graphs.values())
         while total > budget and len(self._graphs) > 1:
             k = next(iter(self._graphs))
@@ -613,6 +613,7 @@ class DenseGGNNChemModel(BtbBatching):
             total -= cs.nbytes()
             cs.release()
             self.graph_stats["evicted"] += 1
+        self.graph_stats["cache_bytes"] = int(total)
 
     def _forward_eval(self, sf, task_id=0):
         """build_loss's forward without autograd on a _StepFeed: front-end ->

@@ -44,3 +44,34 @@ def test_edge_arrays_concatenate_and_validate():
         edge_arrays([[[0, 4, 1]]], 4, 3)        # label outside 1..E (the reference indexes out of range)
     with pytest.raises(IndexError):
         edge_arrays([[[0, 1, 4]]], 4, 3)        # node outside 0..v-1
+
+
+def test_captured_step_cache_evicts_least_recently_used():
+    """model._evict_graphs: while the captured steps hold more than
+    params['hip_graph_cache_mb'], the least recently used one is released
+    (never the step that just ran)."""
+    from collections import OrderedDict
+    from test_dist import _golden_model
+
+    class Fake:
+        def __init__(self, mb):
+            self.mb, self.released = mb, False
+
+        def nbytes(self):
+            return self.mb * 2 ** 20
+
+        def release(self):
+            self.released = True
+
+    m, _ = _golden_model()
+    m.params["hip_graph_cache_mb"] = 10
+    steps = {k: Fake(4) for k in "abcd"}
+    m._graphs = OrderedDict(steps)
+    m._graphs.move_to_end("a")            # "a" ran most recently but one
+    m._graphs.move_to_end("d")
+    m._evict_graphs(keep="d")
+    assert list(m._graphs) == ["a", "d"] and steps["b"].released and steps["c"].released
+    assert m.graph_stats["evicted"] == 2 and m.graph_stats["cache_bytes"] == 8 * 2 ** 20
+    m.params["hip_graph_cache_mb"] = 1
+    m._evict_graphs(keep="a")             # one step always stays: the one that ran
+    assert list(m._graphs) == ["a"] and not steps["a"].released
