@@ -842,9 +842,14 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
     if (a.count == PACK_MAXJ) flush();
     PackJob& J = a.j[a.count];
-    // (one thread per 4-row quad of a column, k_pack_multi; a partial last quad when H % 4 != 0)
-    if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
-    J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop;
+    // mode 2: 16-byte pieces when H % 4 == 0 and both ends are 16-byte aligned
+    // (masked: one thread per 4-row quad of 4 columns); else one thread per
+    // element, or per 4-row quad of a column when masked (a partial last quad
+    // when H % 4 != 0)
+    const int vec = mode == 2 && H % 4 == 0 && !(((uintptr_t)S | (uintptr_t)out) & 15);
+    if (mode == 2 && vec) n = drop ? (long)c.C * (H / 4) * (H / 4) : n / 4;
+    else if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
+    J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop; J.trans = vec;
     a.blk_begin[a.count++] = nb;
     nb += (int)((n + 255) / 256);
   };

@@ -455,6 +455,34 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     return;
   }
   if (J.copy == 2) {  // fp32 copy of W [C][H][H] (H = J.K), edge-dropout mask of timestep J.t when J.drop
+    if (J.trans) {
+      // 16-byte pieces (the host sets trans when H % 4 == 0 and both ends are
+      // 16-byte aligned): unmasked, J.total = C*H*H/4 float4s; masked, one
+      // thread per 4-row quad of 4 columns (J.total = C*(H/4)*(H/4)): the
+      // same Philox block per (c, row quad, column) as the scalar form
+      if (!J.drop) {
+        ((float4*)J.out)[q] = ((const float4*)J.S)[q];
+        return;
+      }
+      const int H = J.K, h4 = H >> 2;
+      const int j4 = (int)(q % h4), iq = (int)((q / h4) % h4), c = (int)(q / ((long)h4 * h4));
+      const long e0 = ((long)c * H + 4 * iq) * H + 4 * j4;
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(J.S + e0 + (long)u * H);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 w = edge_words(dr, c, 4 * iq, 4 * j4 + k, J.t);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float* x = (float*)&v[u] + k;
+          *x = drop_apply(dr, u4_get(w, u), *x);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) *(float4*)((float*)J.out + e0 + (long)u * H) = v[u];
+      return;
+    }
     if (!J.drop) {
       ((float*)J.out)[q] = J.S[q];
       return;

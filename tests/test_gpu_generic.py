@@ -384,3 +384,36 @@ def test_sparse_pairs_rejected_for_dense_staging_and_too_many_edges():
     assert rc == -2
     bad = _lib.dims(b, v, 66, C, 1, True, "fp32", sparse_pairs=True)
     assert lib.ggnn_check_dims(ctypes.byref(bad)) == -2     # hidden % 4 != 0
+
+
+@pytest.mark.parametrize("h,keep", [(400, 0.85), (400, 1.0), (96, 0.5)])
+def test_pack_general_copies_vector_form_equals_scalar_form(h, keep):
+    """ggnn_pack_weights' fp32 W copies (general path, masked per timestep
+    under edge dropout): the 16-byte form (aligned W, hidden % 4 == 0) writes
+    the same bytes as the per-element form (a W 4 bytes off alignment)."""
+    import torch
+    from ggnn_amd.engine import PropagationEngine
+    C, T = 5, 3
+    dev = torch.device("cuda", 0)
+    eng = PropagationEngine(h, C, device=dev, force_generic=True)
+    g = torch.Generator().manual_seed(7)
+    w = {"edge_weights": torch.randn(C, h, h, generator=g), "edge_biases": torch.randn(C, 1, h, generator=g),
+         "gates_kernel": torch.randn(2 * h, 2 * h, generator=g), "gates_bias": torch.randn(2 * h, generator=g),
+         "candidate_kernel": torch.randn(2 * h, h, generator=g), "candidate_bias": torch.randn(h, generator=g)}
+    w = {k: v.to(dev) for k, v in w.items()}
+    big = torch.empty(C * h * h + 1, device=dev)
+    big[1:] = w["edge_weights"].reshape(-1)
+    w_off = dict(w, edge_weights=big[1:].view(C, h, h))
+    assert w_off["edge_weights"].data_ptr() % 16 == 4
+    pa = eng.pack_weights(w, T=T, edge_keep=keep, seed=12345)
+    pb = eng.pack_weights(w_off, T=T, edge_keep=keep, seed=12345)
+    torch.cuda.synchronize()
+    al = lambda x: (x + 255) & ~255  # noqa: E731  (ggnn_api.hip pack_layout)
+    g_w = al(C * h * 4) + al(2 * h * 4) + al(h * 4)
+    n = C * h * h * 4
+    for t in range(T if keep < 1 else 1):
+        o = g_w + t * al(n)
+        a, b = pa.buf[o:o + n], pb.buf[o:o + n]
+        assert torch.equal(a, b), "timestep %d: vector and scalar copies differ" % t
+    if keep == 1.0:
+        assert torch.equal(pa.buf[g_w:g_w + n].view(torch.float32), w["edge_weights"].reshape(-1))
