@@ -260,9 +260,17 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
                             hipStream_t s) {
   const GenAdjL L = gen_adj_layout(c);
   Prof p(K_ADJ, s);
-  fill_async(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s);
-  fill_async(P<u16>(adj, L.AgT), 0, (size_t)c.b * c.C * c.vin * L.vp * 2, s);
-  fill_async(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C, s);
+  // every buffer this staging clears, in one launch (prow / pdeg are read
+  // only by k_pair_fill below)
+  FillSet fs;
+  fs.add(P<u16>(adj, L.Ag), 0, (size_t)c.b * c.C * c.vin * L.vp * 2);
+  fs.add(P<u16>(adj, L.AgT), 0, (size_t)c.b * c.C * c.vin * L.vp * 2);
+  fs.add(P<unsigned char>(adj, L.occ), 0, (size_t)c.b * c.C);
+  if (c.sparse) {
+    fs.add(P<int>(adj, L.prow), 0xFF, (size_t)c.pcap * 4);
+    fs.add(P<float>(adj, L.pdeg), 0, (size_t)c.pcap * 4);
+  }
+  fs.launch(s);
   if (ne > 0)
     hipLaunchKernelGGL(k_gen_adj_edges, dim3((unsigned)std::min(c.b, 4096)), dim3(256), 0, s, edges, goff, c.b, c.vin,
                        L.vp, E, c.prec != PREC_BF16 ? 1 : 0, P<u16>(adj, L.Ag), P<u16>(adj, L.AgT),
@@ -277,8 +285,6 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
     hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
                        P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
                        P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask));
-    fill_async(P<int>(adj, L.prow), 0xFF, (size_t)c.pcap * 4, s);
-    fill_async(P<float>(adj, L.pdeg), 0, (size_t)c.pcap * 4, s);
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
                        P<int>(adj, L.prow), P<float>(adj, L.pdeg));

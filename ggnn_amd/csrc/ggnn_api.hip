@@ -291,6 +291,22 @@ void fill_async(void* p, unsigned char byte, size_t nbytes, hipStream_t s) {
   hipLaunchKernelGGL(k_fill, dim3(grid1d((long)((nbytes + 15) / 16))), dim3(256), 0, s, (unsigned char*)p, nbytes,
                      (unsigned)byte);
 }
+// up to FILL_MAXJ fills as one launch (empty fills skipped)
+struct FillSet {
+  FillJobs f;
+  int count = 0;
+  size_t maxn = 0;
+  void add(void* p, unsigned char byte, size_t nbytes) {
+    if (!nbytes) return;
+    f.p[count] = (unsigned char*)p; f.n[count] = nbytes; f.byte[count] = byte;
+    ++count;
+    maxn = std::max(maxn, nbytes);
+  }
+  void launch(hipStream_t s) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_fill_multi, dim3(grid1d((long)((maxn + 15) / 16)), count), dim3(256), 0, s, f);
+  }
+};
 void copy_async(float* dst, const float* src, long n, hipStream_t s) {
   if (n <= 0) return;
 #ifdef GGNN_PROBE_MEMSET_NODES

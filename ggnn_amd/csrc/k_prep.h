@@ -535,7 +535,7 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
 // captured from a stream were seen to race with their neighbouring kernels on
 // replay).  k_fill: n bytes of `byte` at p (any alignment; 16-byte pieces over
 // the aligned middle, single bytes at the ends)
-__global__ void __launch_bounds__(256) k_fill(unsigned char* __restrict__ p, size_t n, unsigned byte) {
+__device__ __forceinline__ void fill_bytes(unsigned char* __restrict__ p, size_t n, unsigned byte) {
   const size_t mis = (size_t)((16 - ((uintptr_t)p & 15)) & 15);
   const size_t head = mis < n ? mis : n;
   const size_t body = (n - head) & ~(size_t)15;
@@ -547,6 +547,20 @@ __global__ void __launch_bounds__(256) k_fill(unsigned char* __restrict__ p, siz
   if (tid < head) p[tid] = (unsigned char)byte;
   const size_t t0 = head + body;
   if (tid < n - t0) p[t0 + tid] = (unsigned char)byte;
+}
+__global__ void __launch_bounds__(256) k_fill(unsigned char* __restrict__ p, size_t n, unsigned byte) {
+  fill_bytes(p, n, byte);
+}
+// several fills in one launch (blockIdx.y = fill): the staging of one batch
+// clears up to five buffers, each a ~5 us launch on its own
+#define FILL_MAXJ 8
+struct FillJobs {
+  unsigned char* p[FILL_MAXJ];
+  size_t n[FILL_MAXJ];
+  unsigned byte[FILL_MAXJ];
+};
+__global__ void __launch_bounds__(256) k_fill_multi(FillJobs f) {
+  fill_bytes(f.p[blockIdx.y], f.n[blockIdx.y], f.byte[blockIdx.y]);
 }
 // dst[0, n) = src[0, n), fp32 (16-byte pieces when both are 16-byte aligned)
 __global__ void __launch_bounds__(256) k_copy32(float* __restrict__ dst, const float* __restrict__ src, long n) {
