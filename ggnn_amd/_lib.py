@@ -25,7 +25,7 @@ PRECISIONS = ("bf16", "fp16", "fp32")
 # Every symbol include/ggnn.h declares (checked by tests/test_lib.py).
 EXPORTED = (
     "ggnn_version", "ggnn_last_error", "ggnn_check_dims", "ggnn_workspace_bytes",
-    "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_set_adjacency",
+    "ggnn_adjacency_bytes", "ggnn_weight_pack_bytes", "ggnn_pack_weights", "ggnn_pack_weights_batch", "ggnn_set_adjacency",
     "ggnn_set_adjacency_edges",
     "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_heads_workspace_bytes",
@@ -82,6 +82,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         lib.ggnn_weight_pack_bytes.argtypes = [_DP, ctypes.POINTER(ctypes.c_size_t)]
         lib.ggnn_pack_weights.restype = _I
         lib.ggnn_pack_weights.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P]
+        if hasattr(lib, "ggnn_pack_weights_batch"):   # (absent from builds before round 4: A/B runs)
+            lib.ggnn_pack_weights_batch.restype = _I
+            lib.ggnn_pack_weights_batch.argtypes = [_DP, _P, _P, _P, _P, _P, _P, _P, _P, _P]
         lib.ggnn_set_adjacency.restype = _I
         lib.ggnn_set_adjacency.argtypes = [_DP, _P, _P, _P]
         lib.ggnn_set_adjacency_edges.restype = _I

@@ -160,7 +160,8 @@ size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 struct PackL {
   bool fast;
   size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, szW;
-  size_t gW, gszW, gWg, gWc, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc
+  size_t gW, gszW, gWg, gWc, chocc, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc;
+                                            // chocc: the batch's channel occupancy (ggnn_pack_weights_batch)
   long loW, loWg, loWc;  // element offset of the lo part from the hi part
   size_t wf(int t) const { return Wf + (size_t)t * szW; }
   size_t wt(int t) const { return WT + (size_t)t * szW; }
@@ -192,6 +193,7 @@ PackL pack_layout(const Cfg& c) {
   L.gW = o;   o += L.gszW * nW;
   L.gWg = o;  o += al(4 * H * H * 4);
   L.gWc = o;  o += al(2 * H * H * 4);
+  L.chocc = o; o += al(c.C);
   L.total = o;
   return L;
 }
@@ -740,6 +742,73 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
 
 #include "generic_path.h"
 
+int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float* W, const float* beta,
+              const float* Wg, const float* bg, const float* Wc, const float* bc, hipStream_t s) {
+  const PackL L = pack_layout(c);
+  const int H = c.H;
+  PackJobs a;
+  memset(&a, 0, sizeof(a));
+  a.dr = c.edrop;
+  a.chocc = chocc;
+  int nb = 0;
+  auto flush = [&]() {
+    if (!a.count) return;
+    a.blk_begin[a.count] = nb;
+    Prof p(K_PACK, s);
+    if (c.prec != PREC_BF16) hipLaunchKernelGGL(k_pack_multi<true>, dim3(nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pack_multi<false>, dim3(nb), dim3(256), 0, s, a);
+    a.count = 0;
+    nb = 0;
+  };
+  auto job = [&](const float* S, int ldS, long sS, int K, int N, int trans, void* out, long sO, long lo, int batch,
+                 int t, int drop) {
+    if (a.count == PACK_MAXJ) flush();  // (long T under edge dropout)
+    PackJob& J = a.j[a.count];
+    J.S = S; J.out = (u16*)out; J.sS = sS; J.sO = sO; J.lo_off = lo;
+    J.total = (long)batch * (N / 32) * (K / 16) * 64;
+    J.ldS = ldS; J.K = K; J.N = N; J.trans = trans; J.t = t; J.drop = drop; J.copy = 0;
+    a.blk_begin[a.count++] = nb;
+    nb += (int)((J.total + 255) / 256);
+  };
+  auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
+    if (a.count == PACK_MAXJ) flush();
+    PackJob& J = a.j[a.count];
+    // mode 2: 16-byte pieces when H % 4 == 0 and both ends are 16-byte aligned
+    // (masked: one thread per 4-row quad of 4 columns); else one thread per
+    // element, or per 4-row quad of a column when masked (a partial last quad
+    // when H % 4 != 0)
+    const int vec = mode == 2 && H % 4 == 0 && !(((uintptr_t)S | (uintptr_t)out) & 15);
+    if (mode == 2 && vec) n = drop ? (long)c.C * (H / 4) * (H / 4) : n / 4;
+    else if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
+    J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop; J.trans = vec;
+    a.blk_begin[a.count++] = nb;
+    nb += (int)((n + 255) / 256);
+  };
+  if (L.fast) {
+    for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
+      job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
+      job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
+    }
+    job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
+    job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
+    job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
+    job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
+  }
+  copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
+  copy(bg, P<float>(pack, L.bg), 2L * H);
+  copy(bc, P<float>(pack, L.bc), (long)H);
+  // the general path's fp32 operands (generic_path.h), also in a pack made for
+  // the specialised kernels: a pack is made with b = v = 1 dims and may serve a
+  // later general-path batch (v > 128).  Measured cost at config 3: 3.5 MB of
+  // copies, the whole pack launch 0.013 ms per step (profiles/r03b_bench.json)
+  for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
+  copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
+  copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
+  flush();
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -821,6 +890,7 @@ int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes) {
   return GGNN_OK;
 }
 
+
 int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const float* beta, const float* Wg,
                       const float* bg, const float* Wc, const float* bc, ggnn_stream_t stream) {
   Cfg c;
@@ -829,69 +899,31 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack, const float* W, const floa
   if (!pack || !W || !Wg || !bg || !Wc || !bc) return fail(GGNN_EINVAL, "pack_weights: NULL pointer");
   if ((c.flags & GGNN_USE_EDGE_BIAS) && !beta)
     return fail(GGNN_EINVAL, "pack_weights: edge_biases NULL with USE_EDGE_BIAS");
+  return pack_impl(c, pack, nullptr, W, beta, Wg, bg, Wc, bc, (hipStream_t)stream);
+}
+
+int ggnn_pack_weights_batch(const ggnn_dims* d, void* pack, const void* adj, const float* W, const float* beta,
+                            const float* Wg, const float* bg, const float* Wc, const float* bc,
+                            ggnn_stream_t stream) {
+  Cfg c;
+  int e = make_cfg(d, &c);
+  if (e) return e;
+  if (!pack || !adj || !W || !Wg || !bg || !Wc || !bc) return fail(GGNN_EINVAL, "pack_weights_batch: NULL pointer");
+  if ((c.flags & GGNN_USE_EDGE_BIAS) && !beta)
+    return fail(GGNN_EINVAL, "pack_weights_batch: edge_biases NULL with USE_EDGE_BIAS");
   hipStream_t s = (hipStream_t)stream;
-  const PackL L = pack_layout(c);
-  const int H = c.H;
-  PackJobs a;
-  memset(&a, 0, sizeof(a));
-  a.dr = c.edrop;
-  int nb = 0;
-  auto flush = [&]() {
-    if (!a.count) return;
-    a.blk_begin[a.count] = nb;
+  const unsigned char* chocc = nullptr;
+  if (c.generic && c.ed) {
+    // the general path reads W_c only for channels with an edge in the batch
+    // (the tiles / pairs of the others are empty): mask only those copies
+    const PackL L = pack_layout(c);
+    unsigned char* oc = P<unsigned char>(pack, L.chocc);
     Prof p(K_PACK, s);
-    if (c.prec != PREC_BF16) hipLaunchKernelGGL(k_pack_multi<true>, dim3(nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_pack_multi<false>, dim3(nb), dim3(256), 0, s, a);
-    a.count = 0;
-    nb = 0;
-  };
-  auto job = [&](const float* S, int ldS, long sS, int K, int N, int trans, void* out, long sO, long lo, int batch,
-                 int t, int drop) {
-    if (a.count == PACK_MAXJ) flush();  // (long T under edge dropout)
-    PackJob& J = a.j[a.count];
-    J.S = S; J.out = (u16*)out; J.sS = sS; J.sO = sO; J.lo_off = lo;
-    J.total = (long)batch * (N / 32) * (K / 16) * 64;
-    J.ldS = ldS; J.K = K; J.N = N; J.trans = trans; J.t = t; J.drop = drop; J.copy = 0;
-    a.blk_begin[a.count++] = nb;
-    nb += (int)((J.total + 255) / 256);
-  };
-  auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
-    if (a.count == PACK_MAXJ) flush();
-    PackJob& J = a.j[a.count];
-    // mode 2: 16-byte pieces when H % 4 == 0 and both ends are 16-byte aligned
-    // (masked: one thread per 4-row quad of 4 columns); else one thread per
-    // element, or per 4-row quad of a column when masked (a partial last quad
-    // when H % 4 != 0)
-    const int vec = mode == 2 && H % 4 == 0 && !(((uintptr_t)S | (uintptr_t)out) & 15);
-    if (mode == 2 && vec) n = drop ? (long)c.C * (H / 4) * (H / 4) : n / 4;
-    else if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
-    J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop; J.trans = vec;
-    a.blk_begin[a.count++] = nb;
-    nb += (int)((n + 255) / 256);
-  };
-  if (L.fast) {
-    for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
-      job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
-      job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
-    }
-    job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
-    job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
-    job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
-    job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
+    hipLaunchKernelGGL(k_chan_any, dim3((c.C + 255) / 256), dim3(256), 0, s,
+                       P<const unsigned char>(adj, gen_adj_layout(c).occ), c.b, c.C, oc);
+    chocc = oc;
   }
-  copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
-  copy(bg, P<float>(pack, L.bg), 2L * H);
-  copy(bc, P<float>(pack, L.bc), (long)H);
-  // the general path's fp32 operands (generic_path.h), also in a pack made for
-  // the specialised kernels: a pack is made with b = v = 1 dims and may serve a
-  // later general-path batch (v > 128).  Measured cost at config 3: 3.5 MB of
-  // copies, the whole pack launch 0.013 ms per step (profiles/r03b_bench.json)
-  for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
-  copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
-  copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
-  flush();
-  LAUNCHCHK();
-  return GGNN_OK;
+  return pack_impl(c, pack, chocc, W, beta, Wg, bg, Wc, bc, s);
 }
 
 int ggnn_dropout_mask(const ggnn_dims* d, int kind, int t, uint8_t* mask, ggnn_stream_t stream) {

@@ -303,16 +303,32 @@ __global__ void k_pair_reduce_x(const int* __restrict__ pidx, const float* __res
     const int* cl = chl + (long)g * (C + 1);
     const int n = cl[0];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int u = 0; u < n; ++u) {
-      const int c = cl[1 + u];
-      const int p = pidx[(long)c * N + r];
-      if (p < 0) continue;
-      const float4 z = *(const float4*)(Z + (long)p * H + k);
-      acc.x += z.x; acc.y += z.y; acc.z += z.z; acc.w += z.w;
-      if (beta) {
-        const float d = pdeg[p];
-        const float4 bb = *(const float4*)(beta + (long)c * H + k);
-        acc.x += d * bb.x; acc.y += d * bb.y; acc.z += d * bb.z; acc.w += d * bb.w;
+    // 8 channels per step: their pair lookups, then their Z / deg / beta loads,
+    // all issued before the first add (a sentence graph has ~27 channels and
+    // ~3 pairs per row: one dependent lookup-then-load per channel was the
+    // kernel's latency); the adds stay in ascending channel order
+    for (int u0 = 0; u0 < n; u0 += 8) {
+      int cc[8], pp[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cc[j] = u0 + j < n ? cl[1 + u0 + j] : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pp[j] = u0 + j < n ? pidx[(long)cc[j] * N + r] : -1;
+      float4 z[8];
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const long q = pp[j] < 0 ? 0 : pp[j];
+        z[j] = *(const float4*)(Z + q * H + k);
+        d[j] = beta ? pdeg[q] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (pp[j] < 0) continue;
+        acc.x += z[j].x; acc.y += z[j].y; acc.z += z[j].z; acc.w += z[j].w;
+        if (beta) {
+          const float4 bb = *(const float4*)(beta + (long)cc[j] * H + k);
+          acc.x += d[j] * bb.x; acc.y += d[j] * bb.y; acc.z += d[j] * bb.z; acc.w += d[j] * bb.w;
+        }
       }
     }
     *(float4*)(X + r * H + k) = acc;

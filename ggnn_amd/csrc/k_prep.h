@@ -441,7 +441,21 @@ struct PackJobs {
   int blk_begin[PACK_MAXJ + 1];
   int count;
   Drop dr;
+  // ggnn_pack_weights_batch: per-channel occupancy of the staged batch; the
+  // masked fp32 copies (general path, edge dropout) skip channels nobody uses
+  const unsigned char* chocc;
 };
+
+// chocc[c] = 1 iff some graph of the staged batch has an edge in channel c
+// (occ: the general path's [b][C] tile occupancy)
+__global__ void __launch_bounds__(256) k_chan_any(const unsigned char* __restrict__ occ, int b, int C,
+                                                  unsigned char* __restrict__ chocc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  unsigned char f = 0;
+  for (int g = 0; g < b && !f; ++g) f = occ[(long)g * C + c];
+  chocc[c] = f;
+}
 template <bool F16>
 __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
   const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
@@ -466,6 +480,7 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
       }
       const int H = J.K, h4 = H >> 2;
       const int j4 = (int)(q % h4), iq = (int)((q / h4) % h4), c = (int)(q / ((long)h4 * h4));
+      if (a.chocc && !a.chocc[c]) return;  // a channel the staged batch does not use
       const long e0 = ((long)c * H + 4 * iq) * H + 4 * j4;
       float4 v[4];
 #pragma unroll
@@ -492,6 +507,7 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     // whose 4 masks are the 4 words of one Philox block
     const int H = J.K, hq = (H + 3) >> 2;
     const int wj = (int)(q % H), iq = (int)((q / H) % hq), c = (int)(q / ((long)H * hq));
+    if (a.chocc && !a.chocc[c]) return;
     const uint4 w = edge_words(dr, c, 4 * iq, wj, J.t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

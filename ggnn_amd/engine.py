@@ -53,6 +53,7 @@ class WeightPack:
     edge_keep: float = 1.0
     seed: int = 0
     seed_device: bool = False   # seed is the address of a device uint64 (GGNN_SEED_DEVICE)
+    batch_gen: int | None = None  # made for the staged batch of this generation (pack_weights(batch=True))
 
 
 class PropagationEngine:
@@ -101,6 +102,7 @@ class PropagationEngine:
         self._batch = None          # (b, v) of the staged adjacency
         self._ws = {}               # (b, v, T, training) -> workspace
         self._trained = None        # (b, v, T, pack, ws) of the last training forward
+        self._adj_gen = 0           # bumped by every staging (set_adjacency*)
         self.generation = 0         # bumped by every forward (autograd staleness check)
 
     # ------------------------------------------------------------------ utils
@@ -125,14 +127,17 @@ class PropagationEngine:
 
     # ---------------------------------------------------------------- weights
     def pack_weights(self, weights: dict, T: int = 1, edge_keep: float = 1.0, seed: int = 0,
-                     seed_device: bool = False) -> WeightPack:
+                     seed_device: bool = False, batch: bool = False) -> WeightPack:
         """weights: dict of fp32 device tensors with the reference's shapes:
         edge_weights [C,h,h], edge_biases [C,1,h] (or [C,h]), gates_kernel [2h,2h],
         gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h].
         edge_keep < 1: edge-weight dropout (chem_tensorflow_dense.py:397-403),
         one fresh mask per timestep of a T-step pass, keyed by seed.
         seed_device: seed is the address of a device uint64 holding the seed
-        (read when the kernels run: hipGraph capture, ggnn_amd/graphs.py)."""
+        (read when the kernels run: hipGraph capture, ggnn_amd/graphs.py).
+        batch: pack for the batch staged now (ggnn_pack_weights_batch): under
+        edge dropout on the general path only the channels the batch uses get
+        their masked copies; the pack then serves that staged batch only."""
         h, C = self.h, self.C
         _require(weights["edge_weights"], (C, h, h), "edge_weights")
         eb = weights.get("edge_biases") if self.use_edge_bias else None
@@ -145,14 +150,19 @@ class PropagationEngine:
         _require(weights["candidate_kernel"], (2 * h, h), "candidate_kernel")
         _require(weights["candidate_bias"], (h,), "candidate_bias")
         T = int(T) if edge_keep < 1.0 else 1
-        d = self.dims(1, 1, T, edge_keep=edge_keep, seed=seed, seed_device=seed_device)
+        for_batch = bool(batch) and self._batch is not None and edge_keep < 1.0
+        b, v = self._batch if for_batch else (1, 1)
+        d = self.dims(b, v, T, edge_keep=edge_keep, seed=seed, seed_device=seed_device)
         buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)
-        _lib.check(self._lib.ggnn_pack_weights(
-            ctypes.byref(d), _ptr(buf), _ptr(weights["edge_weights"]), _ptr(eb),
-            _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
-            _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream()),
-            "ggnn_pack_weights")
-        return WeightPack(buf, h, C, self.use_edge_bias, T, float(edge_keep), int(seed), bool(seed_device))
+        wp = (_ptr(weights["edge_weights"]), _ptr(eb), _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
+              _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream())
+        if for_batch:
+            _lib.check(self._lib.ggnn_pack_weights_batch(ctypes.byref(d), _ptr(buf), _ptr(self._adj), *wp),
+                       "ggnn_pack_weights_batch")
+        else:
+            _lib.check(self._lib.ggnn_pack_weights(ctypes.byref(d), _ptr(buf), *wp), "ggnn_pack_weights")
+        return WeightPack(buf, h, C, self.use_edge_bias, T, float(edge_keep), int(seed), bool(seed_device),
+                          self._adj_gen if for_batch else None)
 
     # -------------------------------------------------------------- adjacency
     def set_adjacency(self, adjacency: torch.Tensor) -> None:
@@ -171,6 +181,7 @@ class PropagationEngine:
                    "ggnn_set_adjacency")
         self._batch = (int(b), int(v))
         self._trained = None
+        self._adj_gen += 1
 
     def set_adjacency_edges(self, graphs, v: int, num_edge_types: int) -> None:
         """Stage a batch from the reference's edge lists (each graph a list of
@@ -213,6 +224,7 @@ class PropagationEngine:
                                                       n, E, _stream()), "ggnn_set_adjacency_edges")
         self._batch = (int(b), int(v))
         self._trained = None
+        self._adj_gen += 1
 
     def _use_pairs(self, b: int, v: int, n_edges: int) -> bool:
         """Pair mode for this edge-list batch (see __init__'s sparse_pairs)."""
@@ -244,6 +256,9 @@ class PropagationEngine:
         _require(h0, (b, v, self.h), "initial_node_representations")
         if pack.edge_keep < 1.0 and pack.T != T:
             raise ValueError("the pack holds edge-dropout masks for T=%d, forward asked for T=%d" % (pack.T, T))
+        if pack.batch_gen is not None and pack.batch_gen != self._adj_gen:
+            raise RuntimeError("this pack was made for another staged batch (pack_weights(batch=True)): "
+                               "pack again after staging the batch")
         ws = self.workspace(b, v, T, training, pack.edge_keep < 1.0)
         d = self.dims(b, v, T, pack.edge_keep, state_keep, pack.seed, pack.seed_device)
         if out is None:

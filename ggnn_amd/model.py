@@ -86,7 +86,7 @@ class _Propagate(torch.autograd.Function):
         weights = {"edge_weights": W.contiguous(), "edge_biases": beta.contiguous() if beta is not None else None,
                    "gates_kernel": Wg.contiguous(), "gates_bias": bg.contiguous(),
                    "candidate_kernel": Wc.contiguous(), "candidate_bias": bc.contiguous()}
-        pack = engine.pack_weights(weights, T=T, edge_keep=edge_keep, seed=seed)
+        pack = engine.pack_weights(weights, T=T, edge_keep=edge_keep, seed=seed, batch=True)
         # (autograd runs Function.forward with grad mode off: ask the ctx)
         training = any(ctx.needs_input_grad[:7])
         out = engine.forward(h0.contiguous(), pack, T, training=training, state_keep=state_keep)
@@ -634,7 +634,8 @@ class DenseGGNNChemModel(BtbBatching):
                "edge_biases": W["edge_biases"] if self.params["use_edge_bias"] else None,
                "gates_kernel": gru["gates_kernel"], "gates_bias": gru["gates_bias"],
                "candidate_kernel": gru["candidate_kernel"], "candidate_bias": gru["candidate_bias"]}
-        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device)
+        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device,
+                                batch=True)
         hT = eng.forward(h0, pack, T, training=False, state_keep=state_keep)
         self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=sf.seed_values[1])
         keep_o = self._out_keep()
@@ -713,7 +714,8 @@ class DenseGGNNChemModel(BtbBatching):
         wts = {"edge_weights": W["edge_weights"], "edge_biases": beta, "gates_kernel": gru["gates_kernel"],
                "gates_bias": gru["gates_bias"], "candidate_kernel": gru["candidate_kernel"],
                "candidate_bias": gru["candidate_bias"]}
-        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device)
+        pack = eng.pack_weights(wts, T=T, edge_keep=edge_keep, seed=sf.seeds[1], seed_device=sf.seed_device,
+                                batch=True)
         hT = eng.forward(h0, pack, T, training=True, state_keep=state_keep)
         self.last_dropout = dict(edge_keep=edge_keep, state_keep=state_keep, seed=sf.seed_values[1])
         self.ops["final_node_representations"] = hT

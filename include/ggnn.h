@@ -155,6 +155,19 @@ int ggnn_pack_weights(const ggnn_dims* d, void* pack,
                       const float* candidate_kernel, const float* candidate_bias,
                       ggnn_stream_t stream);
 
+/* The same pack for the batch staged in `adj` (d: that batch's dims).  On the
+ * general path under edge dropout it writes the per-timestep masked copies of
+ * W_c only for the channels with an edge somewhere in the batch (the others
+ * are never read by that batch's forward / backward: tf.nn.dropout of
+ * edge_weights, chem_tensorflow_dense.py:397-403, touches only weights the
+ * batch uses).  Everything else, and other paths, as ggnn_pack_weights.  The
+ * pack then serves THAT staged batch only. */
+int ggnn_pack_weights_batch(const ggnn_dims* d, void* pack, const void* adj,
+                            const float* edge_weights, const float* edge_biases,
+                            const float* gates_kernel, const float* gates_bias,
+                            const float* candidate_kernel, const float* candidate_bias,
+                            ggnn_stream_t stream);
+
 /* Test / tuning hook: D[M][N] = A[M][K] B[K][N], row-major fp32 device
  * buffers, through the general path's MFMA product kernel (k_gemm) in the
  * precision policy of d->flags (other fields of d: any valid dims). */

@@ -274,16 +274,20 @@ def _trees(b, v, E, seed, extra=0):
     return graphs, A
 
 
-def _run_edges(graphs, v, E, h0, w, T, precision="fp32", dhT=None, sparse="auto", dr=None, force_generic=False):
+def _run_edges(graphs, v, E, h0, w, T, precision="fp32", dhT=None, sparse="auto", dr=None, force_generic=False,
+               batch_pack=False):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, h = h0.shape[0], h0.shape[-1]
     eng = PropagationEngine(h, 2 * E, precision=precision, sparse_pairs=sparse, force_generic=force_generic)
     dev = eng.device
     dr = dr or dict(edge_keep=1.0, state_keep=1.0, seed=0)
-    pack = eng.pack_weights({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}, T=T,
-                            edge_keep=dr["edge_keep"], seed=dr["seed"])
-    eng.set_adjacency_edges(graphs, v, E)
+    wd = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
+    if batch_pack:     # the model's order: stage the batch, then pack for it (ggnn_pack_weights_batch)
+        eng.set_adjacency_edges(graphs, v, E)
+    pack = eng.pack_weights(wd, T=T, edge_keep=dr["edge_keep"], seed=dr["seed"], batch=batch_pack)
+    if not batch_pack:
+        eng.set_adjacency_edges(graphs, v, E)
     out = eng.forward(torch.from_numpy(np.ascontiguousarray(h0)).to(dev), pack, T, training=dhT is not None,
                       state_keep=dr["state_keep"])
     res = {"hT": out.cpu().numpy(), "sparse": eng.sparse}
@@ -325,8 +329,9 @@ def test_sparse_pairs_fp32_parity(b, v, h, T, extra, sparse):
         assert _nmax(got[k], dense[k]) <= tol, k
 
 
+@pytest.mark.parametrize("batch_pack", [False, True])
 @pytest.mark.parametrize("ek,sk", [(0.9, 0.9), (0.6, 1.0)])
-def test_sparse_pairs_dropout_fp32_parity(ek, sk):
+def test_sparse_pairs_dropout_fp32_parity(ek, sk, batch_pack):
     """Edge-weight dropout in pair mode: the masked weight copies in the
     products and the mask of timestep t applied in the dW product's epilogue
     (no per-timestep slab), against the oracle's Philox masks."""
@@ -340,11 +345,59 @@ def test_sparse_pairs_dropout_fp32_parity(ek, sk):
     A64, w64 = A.astype(np.float64), _f64(w)
     ref, caches = O.forward(A64, h0.astype(np.float64), w64, T, dropout=dr)
     gref = O.backward(A64, dhT.astype(np.float64), caches, w64)
-    got = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr)
+    got = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr, batch_pack=batch_pack)
     assert got["sparse"]
     assert np.abs(got["hT"] - ref).max() <= FP32_TOL
     for k in GRADS:
         assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
+
+
+def test_batch_pack_masks_only_the_batch_channels():
+    """ggnn_pack_weights_batch (the model's pack: stage, then pack for the
+    batch): under edge dropout on the general path it writes the masked W_c
+    copies only for channels with an edge in the staged batch -- a sentence
+    batch touches about half of the 92.  The step's results equal the full
+    pack's (h_T and dL/dh0 bit for bit; weight gradients up to the order of
+    their fp32 atomics), the skipped copies are left unwritten, and a pack made
+    for one staged batch is refused for the next."""
+    torch = _torch()
+    from ggnn_amd.engine import PropagationEngine
+    b, v, h, T, E = 3, 30, 400, 3, 46
+    graphs, A = _trees(b, v, E, seed=11)
+    used = A.reshape(b, 2 * E, -1).max(axis=(0, 2)) > 0
+    assert 0 < used.sum() < 2 * E
+    rng = np.random.default_rng(4)
+    h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
+    w = O.synthetic_weights(h, 2 * E, seed=6)
+    dhT = rng.standard_normal((b, v, h)).astype(np.float32)
+    dr = dict(edge_keep=0.8, state_keep=0.9, seed=777)
+    full = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr)
+    part = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr, batch_pack=True)
+    for k in ("hT", "h0"):
+        assert np.array_equal(full[k], part[k]), k
+    for k in GRADS[1:]:
+        assert _nmax(part[k], full[k]) <= 1e-6, k
+    # the copies: occupied channels masked exactly as the full pack, the others untouched
+    eng = PropagationEngine(h, 2 * E)
+    wd = {k: torch.from_numpy(np.ascontiguousarray(x)).to(eng.device) for k, x in w.items()}
+    eng.set_adjacency_edges(graphs, v, E)
+    pf = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777)
+    pb = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777, batch=True)
+    pb2 = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777, batch=True)
+    torch.cuda.synchronize()
+    al = lambda x: (x + 255) & ~255  # noqa: E731  (ggnn_api.hip pack_layout: beta, bg, bc, then the copies)
+    C = 2 * E
+    g_w = al(C * h * 4) + al(2 * h * 4) + al(h * 4)
+    n = C * h * h * 4
+    for t in range(T):
+        o = g_w + t * al(n)
+        cf = pf.buf[o:o + n].view(torch.float32).view(C, h * h)
+        cb = pb.buf[o:o + n].view(torch.float32).view(C, h * h)
+        u = torch.from_numpy(used).to(eng.device)
+        assert torch.equal(cf[u], cb[u]), t
+    eng.set_adjacency_edges(graphs[:2], v, E)
+    with pytest.raises(RuntimeError):
+        eng.forward(torch.zeros((2, v, h), device=eng.device), pb2, T)
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])

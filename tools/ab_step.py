@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--trees", action="store_true", help="b=256 dependency trees, v=30, C=92 (real density)")
+    ap.add_argument("--reference", action="store_true",
+                    help="with --trees: the reference's model (hidden 400, T = 4), edge lists staged once, pair mode")
     args = ap.parse_args()
     import torch
     from ggnn_amd import _lib
@@ -38,6 +40,9 @@ def main():
 
     dev = torch.device("cuda", 0)
     b, v, h, C, T = 256, 128, 256, 8, 5
+    if args.reference:
+        args.trees, h, T = True, 400, 4
+    graphs = None
     if args.trees:
         v, C = 30, 92
         rng = np.random.default_rng(13)
@@ -45,9 +50,11 @@ def main():
         pz = 1.0 / np.arange(1, E + 1)
         pz /= pz.sum()
         A = np.zeros((b, C, v, v), np.float32)
+        graphs = []
         for g in range(b):
             n = int(rng.integers(v // 2, v + 1))
             ed = [(int(rng.integers(0, i)), int(rng.choice(E, p=pz)) + 1, i) for i in range(1, n)]
+            graphs.append(ed)
             A[g] = O.graph_to_adj_mat_bd(ed, v, E, dtype=np.float32)
         h0 = rng.uniform(-0.2, 0.2, (b, v, h)).astype(np.float32)
     else:
@@ -66,6 +73,8 @@ def main():
         elif variant.startswith("keep"):
             keep = float("0." + variant[4:])
         eng = PropagationEngine(h, C, device=dev, **kw)
+        if args.reference:
+            eng.set_adjacency_edges(graphs, v, C // 2)      # once, as bench.py's real-density lines
         grads = FlatGradients(h, C, True, device=dev)
         gv = dict(grads.views)
         gv["h0"] = torch.empty((b, v, h), device=dev)
@@ -75,7 +84,8 @@ def main():
         def step():
             n[0] += 1
             pack = eng.pack_weights(w_d, T=T, edge_keep=keep, seed=n[0])
-            eng.set_adjacency(A_d)
+            if not args.reference:
+                eng.set_adjacency(A_d)
             eng.forward(h0_d, pack, T, training=True, out=out, state_keep=keep)
             eng.backward(dhT, gv)
             opt.step([grads.views[k] for k in GRAD_ORDER])
