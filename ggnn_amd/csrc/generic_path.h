@@ -23,11 +23,7 @@ struct GenAdjL {
   // pair mode (GGNN_SPARSE_PAIRS, k_pairs.h)
   size_t degc, pidx, pcnt, poff, prow, pdeg, ptile, pmask, wtl, wmap, wmask;
   size_t rcnt, roff, rlist;  // reverse gather lists of the backward's dh scatter (k_pair_rev)
-  // 128-row super tiles (4 consecutive 32-row tiles of one channel) of the
-  // products Z = Y W_c / dY = dXg W_c^T: first tile (the product's zmap), term
-  // list [1, channel], mask; rmask: the 32-row tiles left to the 32-row launch
-  size_t stile, stl, stmask, rmask;
-  int cap_tiles, zw, cap_st;  // product tiles of the pair-row capacity; dW split-K chunks; super tiles
+  int cap_tiles, zw;  // product tiles of the pair-row capacity; dW split-K chunks
 };
 GenAdjL gen_adj_layout(const Cfg& c) {
   GenAdjL L;
@@ -49,7 +45,6 @@ GenAdjL gen_adj_layout(const Cfg& c) {
   L.cgc = o; o += al((size_t)c.C * L.nch * (L.gch + 1) * 4);
   L.cap_tiles = (int)(c.pcap / PAIR_TILE);
   L.zw = c.sparse ? L.cap_tiles / PAIR_CHUNK + c.C : 0;
-  L.cap_st = L.cap_tiles / PAIR_SUPER;
   if (c.sparse) {
     const size_t N = (size_t)c.b * c.vin;
     L.degc = o;  o += al((size_t)c.C * N * 2);
@@ -66,10 +61,6 @@ GenAdjL gen_adj_layout(const Cfg& c) {
     L.rcnt = o;  o += al(N * 4);
     L.roff = o;  o += al((N + 1) * 4);
     L.rlist = o; o += al((size_t)c.pcap * 4);
-    L.stile = o;  o += al((size_t)std::max(L.cap_st, 1) * 4);
-    L.stl = o;    o += al((size_t)std::max(L.cap_st, 1) * 2 * 4);
-    L.stmask = o; o += al((size_t)std::max(L.cap_st, 1));
-    L.rmask = o;  o += al((size_t)L.cap_tiles);
   }
   L.total = o;
   return L;
@@ -293,8 +284,7 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
                        P<int>(adj, L.pidx), P<int>(adj, L.pcnt));
     hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
                        P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
-                       P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask), L.cap_st, P<int>(adj, L.stile),
-                       P<int>(adj, L.stl), P<unsigned char>(adj, L.stmask), P<unsigned char>(adj, L.rmask));
+                       P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask));
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
                        P<int>(adj, L.prow), P<float>(adj, L.pdeg));
@@ -335,21 +325,9 @@ int gen_pairs_product(const Cfg& c, const GenAdjL& AL, const void* adj, const fl
   z.A = Aop; z.sAp = PAIR_TILE * H; z.sAm = H; z.sAk = 1;
   z.B = W; z.sBq = H * H;
   if (wt) { z.sBk = 1; z.sBn = H; } else { z.sBk = H; z.sBn = 1; }
-  z.D = D; z.sDm = H; z.sDn = 1;
-  z.N = (int)H; z.K = (int)H;
-  // runs of 4 tiles of one channel as 128-row tiles: W_c streams once per 128
-  // pair rows instead of once per 32 (a channel with every node row -- the
-  // prev / next-word channels -- holds b*v pair rows)
-  if (AL.cap_st > 0) {
-    GemmArgs q = z;
-    q.zmap = P<const int>(adj, AL.stile); q.sDp = PAIR_TILE * H;  // zp = the super tile's first tile
-    q.tl = P<const int>(adj, AL.stl); q.ts = 2; q.zmask = P<const unsigned char>(adj, AL.stmask);
-    q.Z = AL.cap_st; q.M = PAIR_SUPER * PAIR_TILE;
-    if (int e = gg_launch<PREC>(q, false, true, wt, kind, s)) return e;
-  }
-  z.sDz = PAIR_TILE * H;
-  z.tl = P<const int>(adj, AL.ptile); z.ts = 2; z.zmask = P<const unsigned char>(adj, AL.rmask);
-  z.Z = AL.cap_tiles; z.M = PAIR_TILE;
+  z.D = D; z.sDz = PAIR_TILE * H; z.sDm = H; z.sDn = 1;
+  z.tl = P<const int>(adj, AL.ptile); z.ts = 2; z.zmask = P<const unsigned char>(adj, AL.pmask);
+  z.Z = AL.cap_tiles; z.M = PAIR_TILE; z.N = (int)H; z.K = (int)H;
   return gg_launch<PREC>(z, false, true, wt, kind, s);
 }
 // channel lists of the staged batch (per graph, per channel); rebuilt by every

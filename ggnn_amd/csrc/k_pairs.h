@@ -27,7 +27,6 @@
 #include "ggnn_common.h"
 
 #define PAIR_TILE 32   // rows per product tile (the ring kernel's 32-row variant)
-#define PAIR_SUPER 4   // tiles per super tile (one 128-row product tile)
 // tiles per split-K term list of the dW product (512 rows; 4 and 8 measured
 // slower: more chunks, more atomics)
 #define PAIR_CHUNK 16
@@ -91,26 +90,20 @@ __global__ void __launch_bounds__(1024) k_pair_scan(const u16* __restrict__ degc
 __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pcnt, int C, int cap_tiles, int zw_cap,
                                                       int* __restrict__ poff, int* __restrict__ ptile,
                                                       unsigned char* __restrict__ pmask, int* __restrict__ wtl,
-                                                      int* __restrict__ wmap, unsigned char* __restrict__ wmask,
-                                                      int cap_st, int* __restrict__ stile, int* __restrict__ stl,
-                                                      unsigned char* __restrict__ stmask,
-                                                      unsigned char* __restrict__ rmask) {
-  __shared__ int soff[CHL_MAXC + 1], cst[CHL_MAXC + 1], sst[CHL_MAXC + 1];
+                                                      int* __restrict__ wmap, unsigned char* __restrict__ wmask) {
+  __shared__ int soff[CHL_MAXC + 1], cst[CHL_MAXC + 1];
   const int tid = threadIdx.x;
   if (tid == 0) {
-    int off = 0, ch = 0, sc = 0;
+    int off = 0, ch = 0;
     for (int c = 0; c < C; ++c) {
       soff[c] = off;
       cst[c] = ch;
-      sst[c] = sc;
       const int t = (pcnt[c] + PAIR_TILE - 1) / PAIR_TILE;
       off += t * PAIR_TILE;
       ch += (t + PAIR_CHUNK - 1) / PAIR_CHUNK;
-      sc += t / PAIR_SUPER;
     }
     soff[C] = off;
     cst[C] = ch;
-    sst[C] = sc;
   }
   __syncthreads();
   for (int c = tid; c <= C; c += blockDim.x) poff[c] = soff[c];
@@ -127,22 +120,9 @@ __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pc
   };
   for (int z = tid; z < cap_tiles; z += blockDim.x) {
     const bool live = z < live_tiles;
-    const int c = live ? find(soff, z * PAIR_TILE) : 0;
     ptile[2 * z] = live ? 1 : 0;
-    ptile[2 * z + 1] = c;
+    ptile[2 * z + 1] = live ? find(soff, z * PAIR_TILE) : 0;
     pmask[z] = live ? 1 : 0;
-    // tiles in a full run of PAIR_SUPER from the channel's first tile go to the
-    // 128-row launch; the rest (the channel's last < PAIR_SUPER) to the 32-row one
-    const int j = z - soff[c] / PAIR_TILE;
-    rmask[z] = live && j >= (sst[c + 1] - sst[c]) * PAIR_SUPER ? 1 : 0;
-  }
-  for (int z = tid; z < cap_st; z += blockDim.x) {
-    const bool live = z < sst[C];
-    const int c = live ? find(sst, z) : 0;
-    stile[z] = live ? soff[c] / PAIR_TILE + (z - sst[c]) * PAIR_SUPER : 0;
-    stl[2 * z] = live ? 1 : 0;
-    stl[2 * z + 1] = c;
-    stmask[z] = live ? 1 : 0;
   }
   for (int z = tid; z < zw_cap; z += blockDim.x) {
     int* q = wtl + (long)z * (1 + PAIR_CHUNK);

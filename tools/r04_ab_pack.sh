@@ -8,4 +8,4 @@ for lib in tools/lib_before.so tools/lib_pack.so ggnn_amd/libggnn.so; do
   GGNN_LIB=$lib timeout -k 10 200 python tools/ab_step.py --reference --variants skip,keep9 --rounds 1 --steps 50
 done
 done
-
+timeout -k 10 300 python -u -m pytest -q --timeout 200 tests/test_gpu_generic.py
