@@ -167,8 +167,7 @@ static bool ring_ok(const GemmArgs& a, bool A16, bool AKC, bool BKC) {
   }
   return true;
 }
-// ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail,
-// 3 k_gemm_ring with a 4-slot ring on 32-row tiles: tools/gemm_ring_probe.py);
+// ggnn_dbg_gemm_ex's kernel choice (0 auto, 1 k_gemm, 2 k_gemm_ring or fail);
 // thread-local, so a forward / backward on another thread never sees it
 static thread_local int g_gemm_force = 0;
 // ring depth: 2 slots (64 KiB: two workgroups per CU) -- measured 1.4-2x
@@ -198,10 +197,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     const bool sc = a.scA != 1.0f || a.scB != 1.0f || a.snum;
 #define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
-    if (BM_ == 32 && g_gemm_force == 3) {                                                                   \
-      if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 4, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
-      else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 4, BM_>), grid, dim3(256), 0, s, a, tm, tn);    \
-    } else if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
+    if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
     else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);    \
   } while (0)
 #define GGR(A16_, AKC_, BKC_)              \

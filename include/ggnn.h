@@ -179,8 +179,7 @@ int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const
  *               (exact values: 0/1 adjacency; f16 in the fp16 / fp32 modes)
  *   b_layout 0: B fp32 [K][N]; 1: B fp32 [N][K]
  *   kernel   0: automatic; 1: k_gemm; 2: k_gemm_ring (GGNN_EINVAL if the
- *               operands do not meet its alignment rules); 3: k_gemm_ring with
- *               a 4-slot ring where it picks 32-row tiles (measurement) */
+ *               operands do not meet its alignment rules) */
 int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int a_layout, const float* B,
                      int b_layout, float* D, int kernel, ggnn_stream_t stream);
 
