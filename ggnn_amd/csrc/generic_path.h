@@ -399,12 +399,9 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     gt.bias = P<float>(pack, PL.bg);
     gt.nterm = 2;
     gt.M = (int)N; gt.N = (int)(2 * H); gt.K = (int)H; gt.epi = GG_EPI_SIGMOID;
+    // r*h in the same epilogue (columns n < H of the gates are r)
+    gt.F = P<float>(ws, L.rh(t)); gt.Fsrc = P<const float>(ws, hin); gt.sFm = H; gt.Fn = (int)H;
     if (int e = gg_launch<PREC>(gt, false, true, false, K_GRU_FWD, s)) return e;
-    {
-      Prof p(K_GRU_FWD, s);
-      hipLaunchKernelGGL(k_gen_rh, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
-                         P<const float>(ws, hin), P<float>(ws, L.rh(t)), N, c.H);
-    }
     // cc = tanh([X, r h] Wc + bc)
     GemmArgs cd = gg_args();
     cd.A = P<float>(ws, L.x(t)); cd.sAq = ((long)L.rh(t) - (long)L.x(t)) / 4; cd.sAm = H; cd.sAk = 1;

@@ -362,6 +362,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           if (a.mode == GG_ATOMIC) atomicAdd(d, x);
           else if (a.mode == GG_ADD) *d += x;
           else *d = x;
+          if (a.F && n < a.Fn) a.F[(long)m * a.sFm + n] = x * a.Fsrc[(long)m * a.sFm + n];
         }
     }
     // column sums (GemmArgs::csum): lanes l and l + 32 hold the same column

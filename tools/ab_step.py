@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--trees", action="store_true", help="b=256 dependency trees, v=30, C=92 (real density)")
     ap.add_argument("--reference", action="store_true",
                     help="with --trees: the reference's model (hidden 400, T = 4), edge lists staged once, pair mode")
+    ap.add_argument("--batch", type=int, default=256, help="graphs per batch (20: run_epoch's batch_size)")
     args = ap.parse_args()
     import torch
     from ggnn_amd import _lib
@@ -39,7 +40,7 @@ def main():
     import ggnn_oracle as O
 
     dev = torch.device("cuda", 0)
-    b, v, h, C, T = 256, 128, 256, 8, 5
+    b, v, h, C, T = args.batch, 128, 256, 8, 5
     if args.reference:
         args.trees, h, T = True, 400, 4
     graphs = None
