@@ -73,6 +73,7 @@ struct GenWsL {
   // timestep, so dW_c = sum_t mask_t (Y_t^T dXg_t) runs as ONE product after
   // the timestep loop; WTL: its term lists, every timestep's tiles of a chunk)
   size_t WTL, pslice;
+  size_t MB;  // edge-dropout keep bits of every timestep (k_edge_bits; pair mode, training)
   size_t py(int t) const { return PY + (size_t)t * pslice * 4; }
   size_t pdx(int t) const { return PDX + (size_t)t * pslice * 4; }
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
@@ -110,6 +111,7 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
       L.PDX = o; o += al((size_t)slices * L.pslice * 4);
       const size_t zw = (c.pcap / PAIR_TILE) / PAIR_CHUNK + c.C;
       L.WTL = o; o += al(zw * (1 + (size_t)c.T * PAIR_CHUNK) * 4);
+      if (c.ed) { L.MB = o; o += al((size_t)c.T * c.C * H * ((H + 31) / 32) * 4); }
     }
   } else {
     L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
@@ -210,6 +212,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else if (AKC && !BKC) GGR(false, true, false);
     else if (AKC && BKC) GGR(false, true, true);
     else if (!AKC && !BKC && a.tgroups > 1) {
+      if (a.dr.thr && !a.mbits) return fail(GGNN_EINVAL, "k_gemm_ring: masked term groups need the mask bits (k_edge_bits)");
       // (a 4-slot ring, three slices in flight at one workgroup per CU, measured
       // slower for the weight-gradient products: 1.37 -> 1.72 ms at the
       // reference configuration)
@@ -399,9 +402,12 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     gt.bias = P<float>(pack, PL.bg);
     gt.nterm = 2;
     gt.M = (int)N; gt.N = (int)(2 * H); gt.K = (int)H; gt.epi = GG_EPI_SIGMOID;
-    // r*h in the same epilogue (columns n < H of the gates are r)
-    gt.F = P<float>(ws, L.rh(t)); gt.Fsrc = P<const float>(ws, hin); gt.sFm = H; gt.Fn = (int)H;
     if (int e = gg_launch<PREC>(gt, false, true, false, K_GRU_FWD, s)) return e;
+    {
+      Prof p(K_GRU_FWD, s);
+      hipLaunchKernelGGL(k_gen_rh, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
+                         P<const float>(ws, hin), P<float>(ws, L.rh(t)), N, c.H);
+    }
     // cc = tanh([X, r h] Wc + bc)
     GemmArgs cd = gg_args();
     cd.A = P<float>(ws, L.x(t)); cd.sAq = ((long)L.rh(t) - (long)L.x(t)) / 4; cd.sAm = H; cd.sAk = 1;
@@ -598,7 +604,19 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     a.tl = P<const int>(ws, L.WTL); a.ts = 1 + (long)c.T * PAIR_CHUNK;
     a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
     a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
-    if (c.ed) { a.dr = c.edrop; a.tgroups = c.T; }
+    if (c.ed) {
+      a.dr = c.edrop; a.tgroups = c.T;
+      // the masks as bits, drawn once per (channel with pairs, timestep, weight)
+      // instead of in every dW tile's epilogue at every timestep
+      const int w32 = (int)((H + 31) / 32);
+      uint32_t* mb = P<uint32_t>(ws, L.MB);
+      {
+        Prof p(K_WGRAD, s);
+        hipLaunchKernelGGL(k_edge_bits, dim3(grid1d((long)c.T * C * H * w32)), dim3(256), 0, s, c.edrop,
+                           P<const int>(adj, AL.pcnt), (int)C, (int)H, c.T, w32, mb);
+      }
+      a.mbits = mb; a.mbw = w32; a.mbC = (int)C;
+    }
     if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
   }
   // GRU weight gradients over all T*N rows at once: z = (row chunk, timestep),

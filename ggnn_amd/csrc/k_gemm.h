@@ -87,12 +87,11 @@ struct GemmArgs {
   // timestep k (not drop_t) at each group's end and banked, so one launch sums
   // mask_t-weighted products over t (the pair-mode dW over all timesteps)
   int tgroups;
-  // if F (one-z products): F[m*sFm + n] = x * Fsrc[m*sFm + n] for the stored
-  // x of columns n < Fn -- the GRU's r*h beside the gates (r = columns < H)
-  float* F;
-  const float* Fsrc;
-  long sFm;
-  int Fn;
+  // TGRP with dropout: the keep masks as bits (k_edge_bits; required, the
+  // kernel draws no Philox words): word ((t*C + zp)*N + n)*mbw + m/32, bit m%32
+  // (mbC = C)
+  const uint32_t* mbits;
+  int mbw, mbC;
 };
 
 // exact power of two S <= t carrying the heads' dZ ~ 1/t into the f16 normal
@@ -368,7 +367,6 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
             if (a.mode == GG_ATOMIC) atomicAdd(d, x);
             else if (a.mode == GG_ADD) *d += x;
             else *d = x;
-            if (a.F && n < a.Fn) a.F[(long)m * a.sFm + n] = x * a.Fsrc[(long)m * a.sFm + n];
           }
       }
       if (a.csum) {

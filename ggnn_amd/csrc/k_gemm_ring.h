@@ -275,25 +275,34 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     }
   };
 
-  // ---- TGRP: group tg (timestep tg) done: bank += mask_tg * acc, acc = 0
+  // ---- TGRP: group tg (timestep tg) done: bank += mask_tg * acc, acc = 0.
+  // The group's mask words (GemmArgs::mbits, drawn by k_edge_bits) are loaded
+  // at its first slice (mw: this lane's 32-row word per accumulator tile);
+  // drawing Philox words here, per 128 x 128 tile and timestep, was most of the
+  // kernel's issue at small batches and spilled at 2 waves per EU
   const int gsz = TGRP ? nit / max(a.tgroups, 1) : 0;
-  auto bank_group = [&](int tg) {
+  uint32_t mw[TGRP ? AM : 1][TGRP ? AN : 1];
+  auto load_masks = [&](int tg) {
 #pragma unroll
-    for (int j = 0; j < AN; ++j) {
-      const int n = n0 + wn * AN * 32 + 32 * j + l32;
-      uint4 dq = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+      for (int j = 0; j < AN; ++j) {
+        const int n = n0 + wn * AN * 32 + 32 * j + l32, mb = m0 + wm * AM * 32 + 32 * i;
+        mw[i][j] = (n < a.N && mb < a.M) ? a.mbits[(((long)tg * a.mbC + zp) * a.N + n) * a.mbw + (mb >> 5)] : 0u;
+      }
+  };
+  auto bank_group = [&]() {
+#pragma unroll
+    for (int j = 0; j < AN; ++j)
 #pragma unroll
       for (int i = 0; i < AM; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * AM * 32 + 32 * i + acc_row(r, hh);
-          if (dr.thr && (r & 3) == 0) dq = edge_words(dr, zp, m, n, tg);  // rows m .. m + 3
           const float x = acc[i][j][r];
-          bank[i][j][r] += dr.thr ? drop_apply(dr, u4_get(dq, r & 3), x) : x;
+          bank[i][j][r] += !a.mbits ? x : ((mw[i][j] >> (acc_row(r, hh) & 31)) & 1u) ? x * dr.scale : 0.0f;
         }
         acc[i][j] = splat(0.f);
       }
-    }
   };
 
   // ---- the ring: slices it+1, it+2 stay in flight while slice it is consumed
@@ -306,10 +315,13 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     for (int it = 0; it < nit; ++it) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
+      // (issued ahead of the slice's DMAs: the compiler's wait before their
+      // use at the group's end is a vmcnt(0) that also covers those)
+      if (a.mbits && live && gsz > 0 && it % gsz == 0) load_masks(it / gsz);
       if (it + 1 < nit) stage(it + 1, (it & 1) ? s0 : s1);
       if (live) {
         compute((it & 1) ? s1 : s0);
-        if (gsz > 0 && (it + 1) % gsz == 0) bank_group((it + 1) / gsz - 1);
+        if (gsz > 0 && (it + 1) % gsz == 0) bank_group();
       }
     }
   } else
@@ -326,7 +338,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
         if (live) {
           compute(slot(u));
           if constexpr (TGRP)
-            if (gsz > 0 && (it + 1) % gsz == 0) bank_group((it + 1) / gsz - 1);
+            if (gsz > 0 && (it + 1) % gsz == 0) bank_group();
         }
       }
     }
@@ -362,7 +374,6 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           if (a.mode == GG_ATOMIC) atomicAdd(d, x);
           else if (a.mode == GG_ADD) *d += x;
           else *d = x;
-          if (a.F && n < a.Fn) a.F[(long)m * a.sFm + n] = x * a.Fsrc[(long)m * a.sFm + n];
         }
     }
     // column sums (GemmArgs::csum): lanes l and l + 32 hold the same column

@@ -120,8 +120,17 @@ __global__ void k_gen_wmask_acc(const float* __restrict__ G, float* __restrict__
   }
 }
 
-// ---- forward element-wise steps (G = sigmoid gates [N][2H] = (r | u); r*h is
-// written by the gates product's epilogue, GemmArgs::F)
+// ---- forward element-wise steps (G = sigmoid gates [N][2H] = (r | u))
+// rh = r * h
+__global__ void k_gen_rh(const float* __restrict__ G, const float* __restrict__ h, float* __restrict__ rh, long N,
+                         int H) {
+  const long total = N * H;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long row = e / H;
+    const int k = (int)(e % H);
+    rh[e] = G[row * 2 * H + k] * h[e];
+  }
+}
 // State-dropout element-wise kernels: one thread per (graph, row quad,
 // column) -- rows unpadded (v = vin), so a graph's last quad may be partial --
 // drawing the quad's 4 masks as one Philox block (counter (i >> 2, k, g, t),
