@@ -197,6 +197,42 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     const dim3 grid((unsigned)nwg);
     Prof p(kind, s);
     const bool sc = a.scA != 1.0f || a.scB != 1.0f || a.snum;
+    // K split over the waves (k_gemm_ks) for one-z products whose 32-row grid
+    // leaves the chip mostly idle and walks >= 8 K slices (the GRU products of a
+    // 20-sentence batch): the narrowest column split whose grid stays within
+    // two workgroups per CU.  (Not for term-listed tiles: over the pair tiles
+    // of a 20-sentence batch 32 x 32 tiles measured slower -- prop_fwd 0.226 ->
+    // 0.249 ms per step, W_c and Y re-read per column block -- and a graph's
+    // channel list would hand the waves other terms under channel skipping,
+    // which must stay bit-identical to the dense loop.)
+    const long kslices = (long)((a.K + 31) / 32) * std::max(a.nterm, 1);
+    int wn = 0;
+    if (!A16 && AKC && !sc && a.tgroups <= 1 && a.Z == 1 && !a.tl) {
+      const int fw = g_gemm_force >= 3 ? 1 << (g_gemm_force - 3) : 0;  // forced: 3 -> WN 1, 4 -> 2, 5 -> 4
+      for (int c = 1; c <= 4 && !fw && small && kslices >= 8 && g_gemm_force != 2; c *= 2)
+        if ((long)((a.M + 31) / 32) * ((a.N + 32 * c - 1) / (32 * c)) <= 512) {
+          wn = c;
+          break;
+        }
+      if (fw) wn = fw;
+    }
+    if (wn) {
+      const int tn32 = (a.N + 32 * wn - 1) / (32 * wn), tm32 = (a.M + 31) / 32;
+      const dim3 g32((unsigned)((long)tn32 * tm32));
+#define GKS(BKC_, WN_) hipLaunchKernelGGL((k_gemm_ks<PREC, BKC_, false, WN_>), g32, dim3(256), 0, s, a, tm32, tn32)
+      if (BKC) {
+        if (wn == 1) GKS(true, 1);
+        else if (wn == 2) GKS(true, 2);
+        else GKS(true, 4);
+      } else {
+        if (wn == 1) GKS(false, 1);
+        else if (wn == 2) GKS(false, 2);
+        else GKS(false, 4);
+      }
+#undef GKS
+      return GGNN_OK;
+    }
+    if (g_gemm_force >= 3) return fail(GGNN_EINVAL, "k_gemm_ks: fp32 k-contiguous A, one z, unscaled operands only");
 #define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
     if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \

@@ -1153,7 +1153,7 @@ int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int
   Cfg c;
   if (int e = make_cfg(d, &c)) return e;
   if (!A || !B || !D || M < 1 || N < 1 || K < 1 || a_layout < 0 || a_layout > 2 || b_layout < 0 || b_layout > 1 ||
-      kernel < 0 || kernel > 2)
+      kernel < 0 || kernel > 5)
     return fail(GGNN_EINVAL, "dbg_gemm_ex: bad arguments");
   GemmArgs a = gg_args();
   const bool akc = a_layout != 1, a16 = a_layout == 2, bkc = b_layout == 1;
@@ -1163,7 +1163,7 @@ int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int
   if (bkc) { a.sBn = K; a.sBk = 1; } else { a.sBn = 1; a.sBk = N; }
   a.D = D; a.sDm = N; a.sDn = 1;
   a.M = M; a.N = N; a.K = K;
-  if (kernel == 2 && !ring_ok(a, a16, akc, bkc)) return fail(GGNN_EINVAL, "dbg_gemm_ex: operands not ring-aligned");
+  if (kernel >= 2 && !ring_ok(a, a16, akc, bkc)) return fail(GGNN_EINVAL, "dbg_gemm_ex: operands not ring-aligned");
   hipStream_t s = (hipStream_t)stream;
   g_gemm_force = kernel;
   int e;

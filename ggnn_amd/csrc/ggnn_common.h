@@ -94,7 +94,10 @@ template <bool F16, bool MIX = GGNN_LIMB_MIX> DEV uint32_t pk_lo(float a, float 
     const uint32_t hi = pk<true>(a, b);
     uint32_t lo;
     asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(a), "v"(hi));
-    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(hi));
+    // (the result is an MFMA A/B operand: the VALU write -> MFMA read wait
+    // states go INSIDE the string, hipcc pads only one state after an asm
+    // statement; with that one, k_gemm_ks read stale limbs in fp32 mode)
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1" : "+v"(lo) : "v"(b), "v"(hi));
     return lo;
   }
   const f32x2v v = {a, b};

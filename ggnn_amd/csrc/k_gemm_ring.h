@@ -383,3 +383,201 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     }
   }
 }
+
+// ---- k_gemm_ks: 32-row tiles whose K slices are split over the waves (same
+// GemmArgs contract; fp32 k-contiguous A).  For products whose 32-row ring
+// grid leaves most CUs idle (the GRU and pair products of a 20-sentence batch:
+// 100-400 workgroups), where a launch takes one workgroup's time and that is
+// a serial walk over K: ~7 us + 0.6 us per 32-deep slice, the slice's cost
+// being one wave's LDS-read -> limb-convert -> dependent-MFMA chain, not its
+// DMA (a 4-slot ring walked at the same rate; profiles/r04l_small_gemm_trace.txt).
+// The 4 waves form WN (columns, 32 each) x WK = 4 / WN (K) groups: wave
+// (wn, wk) walks slices wk, wk + WK, ... of columns n0 + 32 wn through a
+// private 2-slot LDS ring (8 KiB a slot; its own vmcnt plus one barrier a
+// round); the WK partial accumulators of a column block are summed in LDS in
+// a fixed order (deterministic), each of the WK waves storing 16 / WK of
+// every lane's 16 rows.  WN = 1 (32 x 32 tiles) has the shortest walk and
+// re-reads A most; WN = 4 is the ring's 32 x 128 tile without the split.
+//   A image [32 m][32 k]: kc32_off;  B k-contiguous [32 n][32 k]: kc32_off;
+//   B row-contiguous [32 k][32 n]: k-row k at row (k & 7) * 4 + (k >> 3), so the
+//   two lane halves of a fragment read (k and k + 8) sit in opposite bank halves.
+namespace gks {
+DEV int rcs_row(int k) { return (k & 7) * 4 + (k >> 3); }
+}  // namespace gks
+
+template <int PREC, bool BKC, bool SCALE, int WN>
+__global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) {
+  const Drop dr = drop_resolve(a.dr);
+  using namespace gr;
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  constexpr int WK = 4 / WN, SLOT = 8192, HALF = 4096;  // one slot: A image, then B image
+  static_assert(WN == 1 || WN == 2 || WN == 4, "wave split");
+  __shared__ __attribute__((aligned(16))) char ring[4 * 2 * SLOT];
+  const GemmScales gs = gemm_scales(a);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int wn = w % WN, wk = w / WN;
+  int z, mt, ntile;
+  ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  if (z >= a.Z) return;
+  if (a.zmask && !a.zmask[z]) return;
+  const int n0 = ntile * 32 * WN + 32 * wn, m0 = mt * 32;  // n0: this wave's column block
+  const int kc = (a.K + BK - 1) / BK;
+  const int zp = a.zmap ? a.zmap[z] : z / a.zdiv, zq = a.zmap ? 0 : z % a.zdiv;
+  const int nterms = a.tl ? a.tl[(long)z * a.ts] : max(a.nterm, 1);
+  const int nit = nterms * kc;
+  int tl0 = 0, tl1 = 0;
+  if (a.tl) {
+    const int* tz = a.tl + (long)z * a.ts + 1;
+    if (lane < nterms) tl0 = tz[lane];
+    if (64 + lane < nterms) tl1 = tz[64 + lane];
+  }
+  asm volatile("" : "+v"(tl0), "+v"(tl1));
+  const int keff = (int)min((long)a.K, a.Ktot - (long)zp * a.sKp);
+  char* const my = ring + w * 2 * SLOT;
+
+  // this wave's DMA sources (4 A + 4 B chunks a lane) at the term's k = 0
+  const char* pa[4];
+  const char* pb[4];
+  int ka[4], kb[4];
+  int cur = -1;
+  auto term_bases = [&](int e) {
+    const int q = !a.tl ? zq + e
+                  : e < 64 ? __builtin_amdgcn_readlane(tl0, e)
+                  : e < 128 ? __builtin_amdgcn_readlane(tl1, e - 64)
+                            : a.tl[(long)z * a.ts + 1 + e];
+    const bool second = a.A2 && q == 1;
+    const long abase = (long)zp * a.sAp + (second ? 0 : (long)q * a.sAq);
+    const char* A1 = (const char*)(second ? a.A2 : a.A);
+    const long bbase = (long)zp * a.sBp + (long)q * a.sBq;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int qs = g * 64 + lane, row = qs >> 3;
+      ka[g] = ((qs & 7) ^ ((row >> 1) & 7)) << 2;
+      int mg = m0 + row;
+      const char* P = A1;
+      int lim = a.Msplit ? a.Msplit : a.M;
+      if (a.Msplit && mg >= a.Msplit) {
+        P = (const char*)a.Am2;
+        mg -= a.Msplit;
+        lim = a.M - a.Msplit;
+      }
+      pa[g] = P + (abase + (long)min(mg, lim - 1) * a.sAm) * 4;
+      if constexpr (BKC) {
+        kb[g] = ka[g];
+        pb[g] = (const char*)a.B + (bbase + (long)min(n0 + row, a.N - 1) * a.sBn) * 4;
+      } else {
+        kb[g] = (row & 3) * 8 + (row >> 2);  // the k-row this LDS row holds
+        pb[g] = (const char*)a.B + (bbase + (long)min(n0 + 4 * (qs & 7), (a.N - 1) & ~3)) * 4;
+      }
+    }
+  };
+  auto stage = [&](int it, char* buf) {
+    const int e = it / kc, kk0 = (it - e * kc) * BK;
+    if (e != cur) {
+      term_bases(e);
+      cur = e;
+    }
+    const char* zero = (const char*)g_ring_zero;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = kk0 + ka[g];
+      glds16_asm(k < keff ? pa[g] + (long)k * 4 : zero, buf + g * 1024);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = kk0 + kb[g];
+      const char* src = BKC ? pb[g] + (long)k * 4 : pb[g] + (long)k * a.sBk * 4;
+      glds16_asm(k < keff ? src : zero, buf + HALF + g * 1024);
+    }
+  };
+  auto compute = [&](const char* buf, f32x16& acc) {
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int k0 = 16 * s + 8 * hh;
+      float x[8];
+      rd8<true>(buf, l32, k0, x);
+      if constexpr (SCALE)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) x[t] *= gs.sa;
+      const frag ah = pk8<F16>(x), al = SPLIT ? pk8_lo<true>(x) : ah;
+      if constexpr (BKC) {
+        rd8<true>(buf + HALF, l32, k0, x);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = *(const float*)(buf + HALF + gks::rcs_row(k0 + j) * 128 + l32 * 4);
+      }
+      if constexpr (SCALE)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) x[t] *= gs.sb;
+      const frag bh = pk8<F16>(x), bl = SPLIT ? pk8_lo<true>(x) : bh;
+      mma<PREC>(acc, ah, al, bh, bl);
+    }
+  };
+
+  f32x16 acc = splat(0.f);
+  const int mine = nit > wk ? (nit - wk + WK - 1) / WK : 0;  // slices wk, wk + WK, ...
+  const int rounds = (nit + WK - 1) / WK;                     // (wk = 0's count: every wave meets each barrier)
+  if (mine > 0) stage(wk, my);
+  for (int u = 0; u < rounds; ++u) {
+    // slice u of this wave landed: its vmcnt, then a barrier before the reads
+    // (a DMA's LDS write is ordered for ds_read only by the wait AND a barrier
+    // passed after it, cdna_hip_programming.md "Read a staged buffer ...")
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (u + 1 < mine) stage(wk + WK * (u + 1), my + ((u + 1) & 1) * SLOT);
+    if (u < mine) compute(my + (u & 1) * SLOT, acc);
+  }
+  if constexpr (WK > 1) {
+    // partials -> this wave's slot 0 (its DMAs are done, its reads consumed)
+    float* red = (float*)my;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
+    __syncthreads();
+  }
+
+  // ---- epilogue: wave (wn, wk) stores accumulator entries r of quads
+  // wk * 4 / WK .. (wk + 1) * 4 / WK - 1 (rows acc_row(r, hh)) of column block wn
+  const int n = n0 + l32;
+  if (n >= a.N) return;
+  const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
+  const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
+  const float bn = bias ? bias[n] : 0.f;
+  const bool hi_n = a.Nsplit && n >= a.Nsplit;
+  float cs = 0.f;
+#pragma unroll
+  for (int qq = 0; qq < 4 / WK; ++qq) {
+    const int quad = wk * (4 / WK) + qq;
+    const int mq = m0 + acc_row(4 * quad, hh);  // rows mq .. mq + 3
+    uint4 dq = make_uint4(0u, 0u, 0u, 0u);
+    if (dr.thr) dq = edge_words(dr, zp, mq, n, a.drop_t);
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const int r = 4 * quad + r4, m = mq + r4;
+      if (m >= a.M) continue;
+      float v;
+      if constexpr (WK == 1) {
+        v = acc[r];
+      } else {
+        const float* rp = (const float*)ring + wn * (2 * SLOT / 4) + r * 64 + lane;  // wave (wn, 0)
+        constexpr int ST = WN * 2 * SLOT / 4;                                          // next wk
+        if constexpr (WK == 2) v = rp[0] + rp[ST];
+        else v = (rp[0] + rp[ST]) + (rp[2 * ST] + rp[3 * ST]);
+      }
+      float x = gs.alpha * v + bn;
+      if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
+      else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+      if (dr.thr) x = drop_apply(dr, u4_get(dq, r4), x);
+      const long doff = dbase + (long)m * (hi_n && a.sD2m ? a.sD2m : a.sDm) + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+      if (a.E) x *= a.E[doff];
+      cs += x;
+      float* d = (hi_n ? a.D2 : a.D) + doff;
+      if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+      else if (a.mode == GG_ADD) *d += x;
+      else *d = x;
+    }
+  }
+  if (a.csum) {
+    cs += __shfl_xor(cs, 32);
+    if (hh == 0) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+  }
+}

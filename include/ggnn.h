@@ -178,8 +178,11 @@ int ggnn_dbg_gemm(const ggnn_dims* d, int M, int N, int K, const float* A, const
  *   a_layout 0: A fp32 [M][K]; 1: A fp32 [K][M]; 2: A 16-bit limbs [M][K]
  *               (exact values: 0/1 adjacency; f16 in the fp16 / fp32 modes)
  *   b_layout 0: B fp32 [K][N]; 1: B fp32 [N][K]
- *   kernel   0: automatic; 1: k_gemm; 2: k_gemm_ring (GGNN_EINVAL if the
- *               operands do not meet its alignment rules) */
+ *   kernel   0: automatic; 1: k_gemm; 2: k_gemm_ring without the K split
+ *               over waves; 3 / 4 / 5: k_gemm_ks (the K split) with 1 / 2 / 4
+ *               column blocks of 32 (fp32 k-contiguous A).  2-5 return
+ *               GGNN_EINVAL if the operands do not meet the ring's alignment
+ *               rules */
 int ggnn_dbg_gemm_ex(const ggnn_dims* d, int M, int N, int K, const void* A, int a_layout, const float* B,
                      int b_layout, float* D, int kernel, ggnn_stream_t stream);
 

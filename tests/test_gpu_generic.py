@@ -253,6 +253,30 @@ def test_k_gemm_ring_layouts(M, N, K, a_layout, b_layout, precision):
     assert np.all(np.abs(ring - old) <= 2 * bound)
 
 
+@pytest.mark.parametrize("M,N,K", RING_SHAPES + [(700, 800, 800), (33, 37 * 4, 1000), (96, 32, 264)])
+@pytest.mark.parametrize("b_layout", [0, 1])
+@pytest.mark.parametrize("precision", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("kernel", [3, 4, 5])
+def test_k_gemm_ks_against_numpy(M, N, K, b_layout, precision, kernel):
+    """k_gemm_ks (32-row tiles, the K slices split over 4 / 2 / 1 wave groups
+    of 1 / 2 / 4 column blocks, partials summed in a fixed order): fp32-parity
+    mode within 1e-6 of float64 relative to the accumulated magnitude, incl.
+    K < 4 slices (waves without a slice), ragged M / N / K tails; deterministic
+    (two runs bit-identical)."""
+    rng = np.random.default_rng(M * 5 + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    Bop = B if b_layout == 0 else np.ascontiguousarray(B.T)
+    ks = _gemm_ex(A, 0, Bop, b_layout, M, N, K, precision, kernel)
+    again = _gemm_ex(A, 0, Bop, b_layout, M, N, K, precision, kernel)
+    assert np.array_equal(ks, again)
+    ref = A.astype(np.float64) @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+    tol = {"fp32": 1e-6, "fp16": 2e-3, "bf16": 1e-2}[precision]
+    bound = tol * scale + K * 2.0 ** -24
+    assert np.all(np.abs(ks - ref) <= bound), float(np.max(np.abs(ks - ref) / bound))
+
+
 # ---------------------------------------------------------------------------
 # Pair mode (GGNN_SPARSE_PAIRS, k_pairs.h): the general path's sparse message
 # passing over the (node, channel) pairs with an incoming edge.

@@ -1,11 +1,14 @@
-# Round-4 GPU session 6: small-product kernel durations from the kernel trace
-# (tools/small_gemm_trace.sh), and the per-kernel split of the reference
-# configuration's 20-sentence training step under edge dropout (k_edge_bits and
-# the masked dW product).
+# Round-4 GPU session 8: k_gemm_ks with 1 / 2 / 4 column blocks per wave
+# group: the whole GPU suite, kernel-trace durations of one product per split,
+# and the reference configuration A/B against the pre-fusion library.
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 bash tools/small_gemm_trace.sh /tmp/sgt > gpurun_out/r04l_small_gemm_trace.txt 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/r04l_ab -o ab -- \
-  python3 tools/ab_step.py --reference --batch 20 --variants keep9 --rounds 1 --steps 30 > gpurun_out/r04l_ab_keep9.log 2>&1
-cp "$(find /tmp/r04l_ab -name '*kernel_stats.csv' | head -1)" gpurun_out/r04l_ab_keep9_b20_kernel_stats.csv
+timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/ > gpurun_out/r04n_tests.log 2>&1
+for k in 3 4 5; do
+  timeout -k 10 300 bash tools/small_gemm_trace.sh /tmp/sgt$k $k > gpurun_out/r04n_small_gemm_trace_k$k.txt 2>&1
+done
+for b in 20 256; do
+  GGNN_LIB=tools/lib_pack.so timeout -k 10 200 python tools/ab_step.py --reference --batch $b --variants skip,keep9 --rounds 1 --steps 50 >> gpurun_out/r04n_ab.log 2>&1
+  timeout -k 10 200 python tools/ab_step.py --reference --batch $b --variants skip,keep9 --rounds 1 --steps 50 >> gpurun_out/r04n_ab.log 2>&1
+done
