@@ -255,33 +255,38 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, pslot(u), qslot(u));
-  for (int it0 = 0; it0 < nit; it0 += NBUF) {
+  // slice `it` from ring slot u = it % NBUF
+  auto slice = [&](int it, int u) {
+    // slice `it` landed (this wave's DMAs: the two younger slices may stay in flight)
+    if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory");
+    else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice `it` landed; slice it-1 fully read
+    if (it + NBUF - 1 < nit) stage(it + NBUF - 1, pslot((u + NBUF - 1) % NBUF), qslot((u + NBUF - 1) % NBUF));
+    const char* bp = pslot(u);
+    const char* bq = qslot(u);
 #pragma unroll
-    for (int u = 0; u < NBUF; ++u) {
-      const int it = it0 + u;
-      if (it >= nit) break;
-      // slice `it` landed (this wave's DMAs: the two younger slices may stay in flight)
-      if (it + 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory");
-      else if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice `it` landed; slice it-1 fully read
-      if (it + NBUF - 1 < nit) stage(it + NBUF - 1, pslot((u + NBUF - 1) % NBUF), qslot((u + NBUF - 1) % NBUF));
-      const char* bp = pslot(u);
-      const char* bq = qslot(u);
+    for (int s = 0; s < BK / 16; ++s) {
+      frag a[4], bb[2];
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
-        frag a[4], bb[2];
+      for (int i = 0; i < 4; ++i) a[i] = lds_frag(bp, soff(wm * 128 + i * 32 + l32, 2 * s + hh));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = lds_frag(bp, soff(wm * 128 + i * 32 + l32, 2 * s + hh));
+      for (int j = 0; j < 2; ++j) bb[j] = lds_frag(bq, soff(wn * 64 + j * 32 + l32, 2 * s + hh));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bb[j] = lds_frag(bq, soff(wn * 64 + j * 32 + l32, 2 * s + hh));
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma<F16>(a[i], bb[j], acc[i][j]);
-      }
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma<F16>(a[i], bb[j], acc[i][j]);
     }
+  };
+  // whole groups of NBUF slices with no exit test inside the unrolled group
+  // (a per-slice break there cost the dense config-3 product ~5 %), then the
+  // tail a graph list may leave
+  const int nfull = nit - nit % NBUF;
+  for (int it0 = 0; it0 < nfull; it0 += NBUF) {
+#pragma unroll
+    for (int u = 0; u < NBUF; ++u) slice(it0 + u, u);
   }
+  for (int u = 0; u < nit - nfull; ++u) slice(nfull + u, u);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
