@@ -183,6 +183,7 @@ template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
+  if (a.E && a.mode == GG_ADD) return fail(GGNN_EINVAL, "gemm: an E factor with GG_ADD (the epilogue preloads one of them)");
   if (g_gemm_force != 1 && ring_ok(a, A16, AKC, BKC)) {
     // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
     // per-(graph, channel) products of v = 30 sentence graphs), and for

@@ -346,6 +346,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   if (!live) return;  // nothing of this wave's to store (no barrier follows)
 
   // ---- epilogue (as k_gemm)
+  constexpr bool EPI_PRE = !TGRP && !A16;  // (masked dW products: atomics only; adjacency products: kept at 3 workgroups per CU)
   const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
   const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
 #pragma unroll
@@ -355,6 +356,25 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     if (n < a.N) {
       const float bn = bias ? bias[n] : 0.f;
       const bool hi_n = a.Nsplit && n >= a.Nsplit;
+      float* const Dn = hi_n ? a.D2 : a.D;
+      const long sm = hi_n && a.sD2m ? a.sD2m : a.sDm, dn = dbase + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+      // the column's E factors / old D values (GG_ADD) loaded up front: read
+      // one at a time between the stores, each waited for its own round trip
+      // (the compiler cannot move a load past a store that may alias it), 64
+      // serialised latencies per lane at 128 rows (E and GG_ADD never meet:
+      // gg_launch refuses the pair)
+      float pre[EPI_PRE ? AM : 1][16];
+      const bool ld = a.E || a.mode == GG_ADD;
+      if (EPI_PRE && ld) {
+        const float* src = a.E ? a.E : Dn;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = min(m0 + wm * AM * 32 + 32 * i + acc_row(r, hh), a.M - 1);
+            pre[i][r] = src[dn + (long)m * sm];
+          }
+      }
       uint4 dq = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
       for (int i = 0; i < AM; ++i)
@@ -367,12 +387,12 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
           else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
           if (!TGRP && dr.thr) x = drop_apply(dr, u4_get(dq, r & 3), x);
-          const long doff = dbase + (long)m * (hi_n && a.sD2m ? a.sD2m : a.sDm) + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
-          if (a.E) x *= a.E[doff];
+          const long doff = dn + (long)m * sm;
+          if (a.E) x *= EPI_PRE ? pre[EPI_PRE ? i : 0][r] : a.E[doff];
           cs += x;
-          float* d = (hi_n ? a.D2 : a.D) + doff;
+          float* d = Dn + doff;
           if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-          else if (a.mode == GG_ADD) *d += x;
+          else if (a.mode == GG_ADD) *d = (EPI_PRE ? pre[EPI_PRE ? i : 0][r] : *d) + x;
           else *d = x;
         }
     }
@@ -543,6 +563,16 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
   const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
   const float bn = bias ? bias[n] : 0.f;
   const bool hi_n = a.Nsplit && n >= a.Nsplit;
+  float* const Dn = hi_n ? a.D2 : a.D;
+  const long sm = hi_n && a.sD2m ? a.sD2m : a.sDm, dn = dbase + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
+  // E factors / old D values (GG_ADD) loaded up front (as k_gemm_ring)
+  float pre[16 / WK];
+  if (a.E || a.mode == GG_ADD) {
+    const float* src = a.E ? a.E : Dn;
+#pragma unroll
+    for (int e = 0; e < 16 / WK; ++e)
+      pre[e] = src[dn + (long)min(m0 + acc_row(4 * (wk * (4 / WK) + (e >> 2)), hh) + (e & 3), a.M - 1) * sm];
+  }
   float cs = 0.f;
 #pragma unroll
   for (int qq = 0; qq < 4 / WK; ++qq) {
@@ -567,12 +597,12 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
       if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
       else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
       if (dr.thr) x = drop_apply(dr, u4_get(dq, r4), x);
-      const long doff = dbase + (long)m * (hi_n && a.sD2m ? a.sD2m : a.sDm) + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
-      if (a.E) x *= a.E[doff];
+      const long doff = dn + (long)m * sm;
+      if (a.E) x *= pre[4 * qq + r4];
       cs += x;
-      float* d = (hi_n ? a.D2 : a.D) + doff;
+      float* d = Dn + doff;
       if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-      else if (a.mode == GG_ADD) *d += x;
+      else if (a.mode == GG_ADD) *d = pre[4 * qq + r4] + x;
       else *d = x;
     }
   }
