@@ -117,7 +117,11 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   int z, mt, ntile;
   ring_tile(gridDim.x, tm, tn, z, mt, ntile);
   if (z >= a.Z) return;
-  if (a.zmask && !a.zmask[z]) return;
+  // zmask[z]: 0 skip z, 1 live, 2 live and the only z writing its outputs
+  // (GG_ATOMIC then stores: the pair dW chunk that is its channel's only one)
+  const unsigned zm = a.zmask ? a.zmask[z] : 1u;
+  if (!zm) return;
+  const bool sole = zm == 2;
   const int n0 = ntile * BN, m0 = mt * BM;
   // a wave whose whole row or column slice lies past M / N (the last tile of
   // N = 400: 16 of its 128 columns valid) still moves its share of every slice
@@ -391,7 +395,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           if (a.E) x *= EPI_PRE ? pre[EPI_PRE ? i : 0][r] : a.E[doff];
           cs += x;
           float* d = Dn + doff;
-          if (a.mode == GG_ATOMIC) atomicAdd(d, x);
+          if (a.mode == GG_ATOMIC && !sole) atomicAdd(d, x);
           else if (a.mode == GG_ADD) *d = (EPI_PRE ? pre[EPI_PRE ? i : 0][r] : *d) + x;
           else *d = x;
         }

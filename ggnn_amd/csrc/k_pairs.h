@@ -86,7 +86,9 @@ __global__ void __launch_bounds__(1024) k_pair_scan(const u16* __restrict__ degc
 // S3: channel offsets (padded to PAIR_TILE), the per-tile term lists of the
 // products (ptile[2z] = 1 live / 0 dead, ptile[2z+1] = channel; pmask), and the
 // dW product's split-K chunks (wtl[z*(1+PAIR_CHUNK)] = tile count, then the
-// tile indices; wmap[z] = channel; wmask).  One block.
+// tile indices; wmap[z] = channel; wmask: 1 live, 2 live and its channel's
+// only chunk, whose dW tiles are then stored instead of added atomically:
+// fp32 atomics bound the dW product at small batches, ~65 G adds/s).  One block.
 __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pcnt, int C, int cap_tiles, int zw_cap,
                                                       int* __restrict__ poff, int* __restrict__ ptile,
                                                       unsigned char* __restrict__ pmask, int* __restrict__ wtl,
@@ -133,7 +135,7 @@ __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pc
       q[0] = cnt;
       for (int e = 0; e < cnt; ++e) q[1 + e] = t0 + j * PAIR_CHUNK + e;
       wmap[z] = c;
-      wmask[z] = 1;
+      wmask[z] = cst[c + 1] - cst[c] == 1 ? 2 : 1;  // 2: the channel's only chunk (k_gemm_ring stores)
     } else {
       q[0] = 0;
       wmap[z] = 0;
