@@ -1,12 +1,9 @@
-# Round-4 GPU session 16: the GRU weight gradients with the timesteps as terms
-# of one chunk (fewer fp32 atomics per output): the GPU suite, then the
-# reference configuration (b = 20, 256) against the previous library.
+# Round-4 final evidence (r04z): rocprof stats + PMC passes + bench line +
+# smoke (tools/profile_round.sh), then the e2e kernel trace of run_epoch
+# summarised per training batch (the raw trace stays on the box).
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/ > gpurun_out/r04z_tests.log 2>&1
-for b in 20 256; do
-  for lib in tools/lib_prev.so ggnn_amd/libggnn.so; do
-    GGNN_LIB=$lib timeout -k 10 200 python tools/ab_step.py --reference --batch $b --variants skip,keep9 --rounds 1 --steps 50 >> gpurun_out/r04z_ab.log 2>&1
-  done
-done
+bash tools/profile_round.sh r04z
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d /tmp/r04z_e2etrace -o run -- python3 tools/e2e_profile.py --no-cprofile > gpurun_out/r04z_e2etrace.log 2>&1
+python3 tools/trace_batch.py "$(find /tmp/r04z_e2etrace -name '*kernel_trace.csv' | head -1)" > gpurun_out/r04z_e2e_train_batch_kernels.txt 2>&1
