@@ -13,7 +13,11 @@ Weak scaling: every rank owns its own 256-graph batch; value = N*256 / t_step
 with t_step the max over ranks.
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W]
-      (N > 1 under torch.distributed.run, one rank per GPU)
+      N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+      the ranks are torchrun's and WORLD_SIZE must equal N; started plainly,
+      bench.py starts the N ranks itself (spawn_ranks: N fresh child
+      processes, before this process imports torch or touches a GPU) and
+      relays rank 0's JSON line.
 """
 from __future__ import annotations
 
@@ -568,6 +572,93 @@ def load_traffic(precision="fp32"):
     return None
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, timeout_s: float | None = None) -> int:
+    """Start an n-rank job of this script: n child processes with RANK /
+    LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT set
+    as torch.distributed.run sets them (one node, rendezvous on 127.0.0.1), one
+    rank per GPU.  The parent never imports torch and never touches a GPU (the
+    children are fresh processes, not forks or execs of an initialised one).
+    Rank 0's stdout (the JSON line) is relayed to stdout; the other ranks'
+    stdout goes to stderr; stderr is inherited.  If a rank fails, the others
+    are terminated and the exit code is the first failure's (else 0).
+    Replaces the reference's unused tf.distribute.MirroredStrategy
+    (chem_tensorflow_dense.py:1327-1328) with N processes over RCCL."""
+    import subprocess
+    import threading
+    port = _free_port()
+    procs, pumps = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                             stdout=subprocess.PIPE, text=True, bufsize=1)
+        sink = sys.stdout if r == 0 else sys.stderr
+
+        def pump(pp=p, out=sink):
+            for line in pp.stdout:
+                out.write(line)
+                out.flush()
+        th = threading.Thread(target=pump, daemon=True)
+        th.start()
+        procs.append(p)
+        pumps.append(th)
+    t_end = None if timeout_s is None else time.monotonic() + timeout_s
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print("bench.py: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        if t_end is not None and time.monotonic() > t_end and live:
+            print("bench.py: ranks %s still running after %.0f s; stopping them" % (sorted(live), timeout_s),
+                  file=sys.stderr)
+            for q in live:
+                procs[q].terminate()
+            rc = rc or 124
+            t_end = None
+        time.sleep(0.05)
+    for th in pumps:
+        th.join(timeout=5)
+    return rc
+
+
+def launch_rehearsal(args):
+    """--launch-only: the N-rank launch and its process group without the
+    propagation step (no GPU work, runs on CPU with --dist-backend gloo): every
+    rank joins the group and all-reduces its rank's batch size; rank 0 prints
+    one JSON line with the world size and global batch the bench line would
+    carry.  It is not a measurement (no metric, no value)."""
+    import torch
+    import torch.distributed as tdist
+    from ggnn_amd.dist import init_from_env
+    rank, world, _ = init_from_env(args.dist_backend)
+    b = torch.tensor([float(CFG["b"])])
+    if tdist.is_initialized():
+        tdist.all_reduce(b)
+    if rank == 0:
+        print(json.dumps({"launch_rehearsal": True, "n_gpus": world, "world_size": world,
+                          "config": {"global_batch": int(b.item()), "parallelism": "dp%d" % world},
+                          "all_reduce": {"backend": tdist.get_backend() if tdist.is_initialized() else None},
+                          "pid": os.getpid(), "launcher": os.environ.get("GGNN_BENCH_LAUNCHER", "external")}),
+              flush=True)
+    if tdist.is_initialized():
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -592,7 +683,25 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
                     help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
                          "parity mode); fp16 / bf16: single 16-bit MFMA operands (reduced precision)")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="only start the N ranks, make the process group and all-reduce once (no GPU work; "
+                         "the launcher's CPU test)")
+    ap.add_argument("--spawn-timeout", type=float, default=None,
+                    help="seconds after which the self-started ranks are stopped (N > 1 without torchrun)")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # plain `python bench.py --gpus N`: start the N ranks here, before any
+        # torch import or GPU call in this process
+        os.environ["GGNN_BENCH_LAUNCHER"] = "bench.py"
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.spawn_timeout))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE %s: one rank per GPU, the two must agree" % (args.gpus, env_world),
+              file=sys.stderr)
+        sys.exit(2)
+    if args.launch_only:
+        return launch_rehearsal(args)
 
     import torch
     import torch.distributed as tdist
@@ -603,8 +712,6 @@ def main():
     import ggnn_oracle as O  # synthetic input generator; not timed
 
     rank, world, local = init_from_env(args.dist_backend)
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     local = local % max(torch.cuda.device_count(), 1)  # (ranks sharing a GPU: the gloo rehearsal only)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -774,6 +881,8 @@ def main():
                            "bytes_per_step": grads.nbytes,
                            "note": "one all-reduce of the flat fp32 gradient buffer per step (RCCL = backend "
                                    "nccl); none without a process group"},
+            "launcher": os.environ.get("GGNN_BENCH_LAUNCHER", "external (torch.distributed.run)"
+                                       if "WORLD_SIZE" in os.environ else "single process"),
             "ms_per_step_event_instrumented": dt_instr * 1e3,
             "adjacency_feed": feed_cmp,
             "dropout_on": {"edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,

@@ -20,6 +20,11 @@ constexpr int kGbAux = kNT;
 // weight-fragment ring loops: outer loop unrolled by 2 (measured against 1 and
 // full unrolling, which spills at H = 256)
 constexpr int GF_UNROLL = 2, GB_UNROLL = 2;
+// k_gru_bwd's weight-fragment ring depth (k-steps in flight)
+#ifndef GGNN_GB_DEPTH
+#define GGNN_GB_DEPTH 2
+#endif
+constexpr int GB_DEPTH = GGNN_GB_DEPTH;
 
 // gru_bwd elementwise phases: loads of GB_GROUP row quads (x 4 arrays) in flight
 // between scheduling barriers (measured: 4 > 2 > 1; VGPRs stay within budget)
@@ -223,6 +228,28 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 //   [dX2 | dh2] = dzg @ Wg^T                       (K = 2H)
 //   out: dX^T = (dX1 + dX2)^T, dh + dh2 (fp32)
 // ===========================================================================
+// Weight limbs of k_gru_bwd's two products in the fp32-parity mode: WH = the
+// hi limb of Wc^T / Wg^T only (2 MFMAs per k-step and output tile: dz_hi W_hi +
+// dz_lo W_hi; dz stays a hi/lo pair), instead of the hi/lo pair (3 MFMAs).
+// Half the weight fragments streamed from L2 per row tile (1.5 -> 0.75 MiB at
+// H = 256) and a third fewer MFMAs.  Error budget (oracle
+// backward_operand_policy, tests/test_precision_policies.py): max |err| /
+// max |ref| of the seven gradients 1.2e-4 -> 5.1e-4 on configs[2] data at
+// T = 5, against the 1e-3 fp32 bar.
+#ifndef GGNN_GB_WHI
+#define GGNN_GB_WHI 1
+#endif
+template <int PREC, bool WH, typename W>
+DEV void gb_mma(f32x16& a1, f32x16& a2, frag ah, frag al, const W& w) {
+  if constexpr (WH) {
+    mma_xb<PREC>(a1, ah, al, w.a);
+    mma_xb<PREC>(a2, ah, al, w.b);
+  } else {
+    mma<PREC>(a1, ah, al, w.a, w.b);
+    mma<PREC>(a2, ah, al, w.c, w.d);
+  }
+}
+
 template <int H, int RT, int PREC>
 __global__ void __launch_bounds__(2 * H)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
@@ -230,7 +257,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
           float* __restrict__ dh_out, u16* __restrict__ dzcT, u16* __restrict__ dzgT,
           float* __restrict__ dbc, float* __restrict__ dbg, long N, const uint32_t* __restrict__ gmax) {
-  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16, WH = SPLIT && GGNN_GB_WHI;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
   const float ds = gscale(gmax);  // gradient scale of dL/dh_T read in place (ggnn_common.h), else 1
   typedef Swz<ZCH> SZ;
@@ -292,16 +319,17 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) { a1[rt] = splat(0.f); a2[rt] = splat(0.f); }
   auto ld1 = [&](int ks) {
-    return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
-              frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
+    if constexpr (WH) return F2{frag_ld(WcTp, ns, ks, KS, lane), frag_ld(WcTp, NS + ns, ks, KS, lane)};
+    else
+      return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
+                frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
   };
-  b_pipeline<KS, 2, GB_UNROLL>(ld1, [&](int ks, const F4& w) {
+  b_pipeline<KS, GB_DEPTH, GB_UNROLL>(ld1, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      mma<PREC>(a1[rt], ah, al, w.a, w.b);
-      mma<PREC>(a2[rt], ah, al, w.c, w.d);
+      gb_mma<PREC, WH>(a1[rt], a2[rt], ah, al, w);
     }
   });
   __syncthreads();  // dzc reads done
@@ -339,16 +367,18 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 
   // ---- product 2: [dX2 | dh2] = dzg @ Wg^T
   auto ld2 = [&](int ks) {
-    return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
-              frag_ld(WgTp, NS + ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
+    if constexpr (WH) return F2{frag_ld(WgTp, ns, ks, 2 * KS, lane), frag_ld(WgTp, NS + ns, ks, 2 * KS, lane)};
+    else
+      return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
+                frag_ld(WgTp, NS + ns, ks, 2 * KS, lane),
+                SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
   };
-  b_pipeline<2 * KS, 2, GB_UNROLL>(ld2, [&](int ks, const F4& w) {
+  b_pipeline<2 * KS, GB_DEPTH, GB_UNROLL>(ld2, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      mma<PREC>(a1[rt], ah, al, w.a, w.b);
-      mma<PREC>(a2[rt], ah, al, w.c, w.d);
+      gb_mma<PREC, WH>(a1[rt], a2[rt], ah, al, w);
     }
   });
   TSMARK(1, 4);

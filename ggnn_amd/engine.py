@@ -150,7 +150,10 @@ class PropagationEngine:
         _require(weights["candidate_kernel"], (2 * h, h), "candidate_kernel")
         _require(weights["candidate_bias"], (h,), "candidate_bias")
         T = int(T) if edge_keep < 1.0 else 1
-        for_batch = bool(batch) and self._batch is not None and edge_keep < 1.0
+        # (a library built before round 4 has no ggnn_pack_weights_batch: the
+        # whole-set pack is still correct there, only slower)
+        for_batch = (bool(batch) and self._batch is not None and edge_keep < 1.0
+                     and hasattr(self._lib, "ggnn_pack_weights_batch"))
         b, v = self._batch if for_batch else (1, 1)
         d = self.dims(b, v, T, edge_keep=edge_keep, seed=seed, seed_device=seed_device)
         buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)

@@ -298,3 +298,43 @@ def test_model_seeds_the_global_rngs_like_the_reference():
     np.random.seed(0)
     random.seed(0)
     assert (a, b) == (np.random.rand(), random.random())
+
+
+# ---------------------------------------------------------------------------
+# bench.py's own N-rank launch: `python bench.py --gpus N`
+# without torch.distributed.run starts the N ranks itself
+# ---------------------------------------------------------------------------
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=_ROOT, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_bench_starts_its_own_ranks_without_torchrun():
+    import json
+    r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--launch-only"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 512, res
+    assert res["all_reduce"]["backend"] == "gloo" and res["launcher"] == "bench.py"
+
+
+def test_bench_refuses_a_world_size_that_disagrees_with_gpus():
+    r = _bench(["--gpus", "2", "--launch-only"], {"WORLD_SIZE": "3", "RANK": "0"})
+    assert r.returncode == 2 and "must agree" in r.stderr, (r.returncode, r.stderr[-2000:])
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    """Ranks that cannot join (RCCL on a machine without a GPU) fail the whole
+    job with a non-zero exit; no JSON line is relayed."""
+    r = _bench(["--gpus", "2", "--dist-backend", "nccl", "--launch-only"], timeout=120)
+    assert r.returncode != 0 and "exited with" in r.stderr, (r.returncode, r.stderr[-2000:])
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -134,6 +134,23 @@ def test_bench_two_ranks_rehearsal():
     assert res["value"] > 0 and "cpu_baseline" not in res
 
 
+def test_bench_self_started_two_ranks():
+    """`python bench.py --gpus 2` WITHOUT torch.distributed.run (how the driver
+    starts the N = 1 line): bench.py starts both ranks itself (fresh child
+    processes, before any GPU call in the parent), here as two gloo ranks on
+    the one GPU, and relays rank 0's one JSON line with n_gpus = 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-side",
+           "--dist-backend", "gloo", "--spawn-timeout", "240"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 512 and res["config"]["parallelism"] == "dp2"
+    assert res["all_reduce"]["backend"] == "gloo" and res["value"] > 0
+
+
 def test_two_rank_captured_step_returns_the_union_loss(tmp_path):
     """Edge-list feeds with hipGraph-captured steps at world size 2: the
     captured step's loss is summed inside the graph BEFORE the all-reduce,

@@ -5,6 +5,9 @@ profiles/r03_precision_policies.json (CPU only; tests/test_precision_policies.py
 asserts the conclusions on a smaller slice).
 
     python tools/precision_policies.py [b]
+    python tools/precision_policies.py --backward [b]   (the fp32-parity backward's
+        weight-limb policies, oracle.backward_operand_policy: all seven gradients,
+        max |err| / max |ref| against the 1e-3 bar; profiles/r05_backward_policies.json)
 """
 import json
 import os
@@ -46,7 +49,51 @@ def table(A, h0, w, Ts):
     return out
 
 
+BWD_POLICIES = [("f16x2", "f16x2", "f16x2", "f16"), ("f16x2", "f16", "f16x2", "f16"), ("f16x2", "f16x2", "f16", "f16"),
+                ("f16x2", "f16", "f16", "f16"), ("f16", "f16x2", "f16x2", "f16")]
+
+
+def backward_table(A, h0, w, T, seed=14):
+    A, h0 = np.asarray(A, np.float64), np.asarray(h0, np.float64)
+    w = {k: np.asarray(x, np.float64) for k, x in w.items()}
+    out = {}
+    for name, dr in (("no_dropout", None), ("dropout_0.9", dict(edge_keep=0.9, state_keep=0.9, seed=77))):
+        _, caches = O.forward(A, h0, w, T, dropout=dr)
+        dhT = np.random.default_rng(seed).standard_normal(h0.shape)
+        ref = O.backward_operand_policy(A, dhT, caches, w, "exact", "exact", "exact", "exact")
+        rows = {}
+        for pol in BWD_POLICIES:
+            g = O.backward_operand_policy(A, dhT, caches, w, *pol)
+            e = {k: float(np.abs(g[k] - ref[k]).max() / np.abs(ref[k]).max()) for k in ref}
+            rows["act=%s,gru_wt=%s,prop_wt=%s,wgrad=%s" % pol] = {"max_nmax": max(e.values()), "per_gradient": e}
+            print(name, pol, "%.2e" % max(e.values()), flush=True)
+        out[name] = rows
+    return out
+
+
+def main_backward(b):
+    A, h0 = O.synthetic_batch(b, 128, 256, 8, seed=1)
+    w = O.synthetic_weights(256, 8, seed=1)
+    res = {"note": "the fp32-parity backward's MFMA operand roundings (oracle.backward_operand_policy): act = dzc, "
+                   "dzg, dM operands of the dh / dX chain; gru_wt = Wc^T, Wg^T in k_gru_bwd's products; prop_wt = "
+                   "W_c^T in k_prop_bwd's dM W_c^T; wgrad = both operands of the weight-gradient products. Forward "
+                   "caches exact, accumulation float64; value = max over the seven gradients of max |err| / "
+                   "max |ref| (the fp32 bar is 1e-3). Round 5 ships gru_wt=f16 (k_gru_bwd hi limbs only).",
+           "configs[2]_synthetic": {"shape": "b=%d v=128 hidden=256 C=8 T=5, SURVEY §8d seed 1" % b,
+                                    "policies": backward_table(A, h0, w, 5)}}
+    At = trees(b, 30, 46, 3)
+    h0t = np.random.default_rng(4).uniform(-0.2, 0.2, (b, 30, 256))
+    wt = O.synthetic_weights(256, 92, seed=3, parity_bias=False)
+    res["dependency_trees"] = {"shape": "b=%d v=30 hidden=256 E=46 (C=92) T=5, Zipf labels" % b,
+                               "policies": backward_table(At, h0t, wt, 5)}
+    with open(os.path.join(ROOT, "profiles", "r05_backward_policies.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
 def main():
+    if "--backward" in sys.argv:
+        args = [a for a in sys.argv[1:] if a != "--backward"]
+        return main_backward(int(args[0]) if args else 32)
     b = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     A, h0 = O.synthetic_batch(b, 128, 256, 8, seed=1)
     w = O.synthetic_weights(256, 8, seed=1)
