@@ -76,8 +76,10 @@ def kernel_issued_flops(kind, b, v, h, C, T, precision):
         return b * (3 * f["mt"] + 2 * f["agg"])
     if kind == "prop_bwd":
         return b * (3 * f["mt"] + 2 * f["agg"] + dbeta)
-    if kind in ("gru_fwd", "gru_bwd"):
+    if kind == "gru_fwd":
         return 3 * b * f["gru"]
+    if kind == "gru_bwd":   # dz hi/lo x the weights' hi limb only (round 5): 2 products
+        return 2 * b * f["gru"]
     return kernel_algo_flops(kind, b, v, h, C, T)
 
 
@@ -683,6 +685,9 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=("fp32", "fp16", "bf16"),
                     help="fp32: GGNN_FP32_PARITY (matches the reference fp32 math to <= 1e-3, the "
                          "parity mode); fp16 / bf16: single 16-bit MFMA operands (reduced precision)")
+    ap.add_argument("--no-dropout-leg", action="store_true",
+                    help="skip the dropout-on leg (a rocprofv3 run then sees only the dropout-off steps the "
+                         "roofline is computed from)")
     ap.add_argument("--launch-only", action="store_true",
                     help="only start the N ranks, make the process group and all-reduce once (no GPU work; "
                          "the launcher's CPU test)")
@@ -774,14 +779,16 @@ def main():
         barrier()
         dt_instr = (time.perf_counter() - t3) / args.steps
     # the same step with the training-feed dropout (keep 0.9 for both), reported beside
-    for _ in range(args.warmup):
-        step(args.dropout_keep)
-    barrier()
-    t2 = time.perf_counter()
-    for _ in range(args.steps):
-        step(args.dropout_keep)
-    barrier()
-    dt_drop = (time.perf_counter() - t2) / args.steps
+    dt_drop = float("nan")
+    if not args.no_dropout_leg:
+        for _ in range(args.warmup):
+            step(args.dropout_keep)
+        barrier()
+        t2 = time.perf_counter()
+        for _ in range(args.steps):
+            step(args.dropout_keep)
+        barrier()
+        dt_drop = (time.perf_counter() - t2) / args.steps
     if tdist.is_initialized():
         tt = torch.tensor([dt, dt_drop], dtype=torch.float64, device=dev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
@@ -832,6 +839,24 @@ def main():
         roof["frac_issued"] = ifl / (avg_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS
         if ceil:
             roof["frac_issued_of_measured"] = ifl / (avg_ms * 1e-3) / 1e12 / roof["measured_peak"]
+    # the same figures for every MFMA kernel of the step (k_gru_bwd beside the dominant one)
+    roof["kernels"] = {}
+    for k in ("fwd_fused", "gru_bwd", "prop_bwd", "wgrad"):
+        if not timer.launches.get(k):
+            continue
+        am = timer.total_ms[k] / timer.launches[k]
+        afl, ifl_k = kernel_algo_flops(k, b, v, h, C, T), kernel_issued_flops(k, b, v, h, C, T, args.precision)
+        kd = {"avg_launch_ms": am, "launches_per_step": timer.launches[k] / args.steps,
+              "algo_flops_per_launch": afl, "frac": afl / (am * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
+              "issued_flops_per_launch": ifl_k, "frac_issued": ifl_k / (am * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+        if ceil:
+            kd["frac_issued_of_measured"] = ifl_k / (am * 1e-3) / 1e12 / ceil["gemm_bf16_tflops" if
+                                                                             args.precision == "bf16" else
+                                                                             "gemm_f16_tflops"]
+        if tr and k in tr.get("kernels", {}):
+            kd["traffic"] = tr["kernels"][k]["hbm_bytes_per_launch"]
+            kd["hbm_frac"] = kd["traffic"] / (am * 1e-3) / 1e9 / HBM_PEAK_GBS
+        roof["kernels"][k] = kd
     breakdown = {k: {"ms_per_step": timer.total_ms[k] / args.steps, "launches_per_step": timer.launches[k] / args.steps}
                  for k in kinds}
 
@@ -865,10 +890,12 @@ def main():
             "vs_baseline": None,
             "dtype": {"fp32": "fp32", "fp16": "fp16", "bf16": "bf16"}[args.precision],
             "precision_note": {"fp32": "fp32-class: every non-exact MFMA operand of the forward and of the "
-                                       "dh/dX chain as an f16 hi/lo limb pair (3 products), fp32 accumulation; "
-                                       "the weight-gradient GEMMs (k_wgrad256) take SINGLE f16 operands, on a "
-                                       "power-of-two-scaled gradient; parity <= 1e-3 vs the fp32 reference "
-                                       "(tests/test_gpu_parity.py, incl. loss-scale gradients)",
+                                       "dh/dX chain as an f16 hi/lo limb pair (3 products), fp32 accumulation, "
+                                       "except k_gru_bwd's Wc^T / Wg^T (the hi limb only: dz hi/lo x W hi, 2 "
+                                       "products); the weight-gradient GEMMs (k_wgrad256) take SINGLE f16 "
+                                       "operands, on a power-of-two-scaled gradient; parity <= 1e-3 vs the fp32 "
+                                       "reference (tests/test_gpu_parity.py, incl. loss-scale gradients; the "
+                                       "backward's limb policy: tests/test_precision_policies.py)",
                                "fp16": "f16 MFMA operands, fp32 accumulation (reduced precision)",
                                "bf16": "bf16 MFMA operands, fp32 accumulation (reduced precision)"}[args.precision],
             "data": "synthetic (SURVEY §8d generator: Bernoulli(0.1) adjacency on n~U{v/2..v} active nodes, glorot weights)",
@@ -885,7 +912,8 @@ def main():
                                        if "WORLD_SIZE" in os.environ else "single process"),
             "ms_per_step_event_instrumented": dt_instr * 1e3,
             "adjacency_feed": feed_cmp,
-            "dropout_on": {"edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
+            "dropout_on": None if args.no_dropout_leg else {
+                           "edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
                            "value": world * b / dt_drop, "ms_per_step": dt_drop * 1e3,
                            "note": "same step with the reference's training-feed dropout (:860-861); "
                                    "value above is dropout off (keep 1, the parity setting)"},

@@ -280,16 +280,11 @@ int grid1d(long n, int bs = 256) {
   const long g = (n + bs - 1) / bs;
   return (int)std::min<long>(std::max<long>(g, 1), 8192);
 }
-// device-side fill / copy on the stream (kernels: capture-safe, see k_fill).
-// GGNN_PROBE_MEMSET_NODES builds the round-2 form (hipMemsetAsync /
-// hipMemcpyAsync, i.e. memset and memcpy nodes under stream capture) for
-// tools/capture_probe.py only; the library never ships it.
+// device-side fill / copy on the stream (kernels: one kind of graph node
+// under stream capture; tools/build_memset_probe_lib.py builds the round-2
+// hipMemsetAsync / hipMemcpyAsync form for tools/capture_probe.py)
 void fill_async(void* p, unsigned char byte, size_t nbytes, hipStream_t s) {
   if (!nbytes) return;
-#ifdef GGNN_PROBE_MEMSET_NODES
-  (void)hipMemsetAsync(p, byte, nbytes, s);  // (an error surfaces at the next LAUNCHCHK)
-  return;
-#endif
   hipLaunchKernelGGL(k_fill, dim3(grid1d((long)((nbytes + 15) / 16))), dim3(256), 0, s, (unsigned char*)p, nbytes,
                      (unsigned)byte);
 }
@@ -311,10 +306,6 @@ struct FillSet {
 };
 void copy_async(float* dst, const float* src, long n, hipStream_t s) {
   if (n <= 0) return;
-#ifdef GGNN_PROBE_MEMSET_NODES
-  (void)hipMemcpyAsync(dst, src, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
-  return;
-#endif
   hipLaunchKernelGGL(k_copy32, dim3(grid1d((n + 3) / 4)), dim3(256), 0, s, dst, src, n);
 }
 
@@ -913,9 +904,12 @@ int ggnn_pack_weights_batch(const ggnn_dims* d, void* pack, const void* adj, con
     return fail(GGNN_EINVAL, "pack_weights_batch: edge_biases NULL with USE_EDGE_BIAS");
   hipStream_t s = (hipStream_t)stream;
   const unsigned char* chocc = nullptr;
-  if (c.generic && c.ed) {
+  if (c.generic && c.ed && !(c.flags & GGNN_DENSE_CHANNELS)) {
     // the general path reads W_c only for channels with an edge in the batch
-    // (the tiles / pairs of the others are empty): mask only those copies
+    // (the tiles / pairs of the others are empty): mask only those copies.
+    // Not under GGNN_DENSE_CHANNELS: there every (graph, channel) tile is run
+    // (k_gen_lists counts them all), so M = h W_c reads every channel's copy
+    // and an unwritten one would enter the products as 0 * (stale bits)
     const PackL L = pack_layout(c);
     unsigned char* oc = P<unsigned char>(pack, L.chocc);
     Prof p(K_PACK, s);

@@ -127,7 +127,7 @@ class PropagationEngine:
 
     # ---------------------------------------------------------------- weights
     def pack_weights(self, weights: dict, T: int = 1, edge_keep: float = 1.0, seed: int = 0,
-                     seed_device: bool = False, batch: bool = False) -> WeightPack:
+                     seed_device: bool = False, batch: bool = False, out: torch.Tensor | None = None) -> WeightPack:
         """weights: dict of fp32 device tensors with the reference's shapes:
         edge_weights [C,h,h], edge_biases [C,1,h] (or [C,h]), gates_kernel [2h,2h],
         gates_bias [2h], candidate_kernel [2h,h], candidate_bias [h].
@@ -137,7 +137,9 @@ class PropagationEngine:
         (read when the kernels run: hipGraph capture, ggnn_amd/graphs.py).
         batch: pack for the batch staged now (ggnn_pack_weights_batch): under
         edge dropout on the general path only the channels the batch uses get
-        their masked copies; the pack then serves that staged batch only."""
+        their masked copies; the pack then serves that staged batch only.
+        out: a caller-owned uint8 device buffer of at least
+        ggnn_weight_pack_bytes to pack into (else one is allocated)."""
         h, C = self.h, self.C
         _require(weights["edge_weights"], (C, h, h), "edge_weights")
         eb = weights.get("edge_biases") if self.use_edge_bias else None
@@ -156,7 +158,13 @@ class PropagationEngine:
                      and hasattr(self._lib, "ggnn_pack_weights_batch"))
         b, v = self._batch if for_batch else (1, 1)
         d = self.dims(b, v, T, edge_keep=edge_keep, seed=seed, seed_device=seed_device)
-        buf = torch.empty(_lib.weight_pack_bytes(d), dtype=torch.uint8, device=self.device)
+        nbytes = _lib.weight_pack_bytes(d)
+        if out is None:
+            buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        else:
+            if out.dtype != torch.uint8 or out.device.type != "cuda" or out.numel() < nbytes or not out.is_contiguous():
+                raise ValueError("out must be a contiguous uint8 device buffer of >= %d bytes" % nbytes)
+            buf = out
         wp = (_ptr(weights["edge_weights"]), _ptr(eb), _ptr(weights["gates_kernel"]), _ptr(weights["gates_bias"]),
               _ptr(weights["candidate_kernel"]), _ptr(weights["candidate_bias"]), _stream())
         if for_batch:

@@ -138,13 +138,14 @@ class CapturedStep:
         self.graph = None
         self.out = None
         self.runs = 0               # batches this step has run (eager first, then replays)
+        self.pool_bytes = 0         # allocated in the graph's private pool during the capture
 
     def nbytes(self) -> int:
         """Device bytes this step holds: its input buffer, the engine's staged
-        adjacency and workspaces, the heads' workspace and the graph's outputs
-        (the activations the captured body allocates in the graph's private
-        pool are small beside the engine's training workspace)."""
-        n = self.inputs.buf.numel()
+        adjacency and workspaces, the heads' workspace, and what the captured
+        body allocated in the graph's private pool (its activations and
+        outputs: memory_allocated across the capture)."""
+        n = self.inputs.buf.numel() + int(self.pool_bytes)
         eng = self.engine
         if getattr(eng, "_adj", None) is not None:
             n += eng._adj.numel()

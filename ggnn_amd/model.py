@@ -572,10 +572,15 @@ class DenseGGNNChemModel(BtbBatching):
         else:
             if cs.graph is None:             # its second batch: capture, then replay
                 g = torch.cuda.CUDAGraph()
+                before = torch.cuda.memory_allocated(self.device)
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     cs.out = body()          # recorded, not executed
                 cs.graph = g
+                # the activations the captured body allocated live in the
+                # graph's private pool for as long as the graph does
+                cs.pool_bytes = max(torch.cuda.memory_allocated(self.device) - before, 0)
                 self.graph_stats["captured"] += 1
+                self._evict_graphs(keep=key)
             cs.graph.replay()
             out = cs.out
             self.graph_stats["replayed"] += 1
@@ -853,9 +858,17 @@ class DenseGGNNChemModel(BtbBatching):
         ids) of every batch across the ranks; a mismatch raises instead of
         silently training some batches twice and others never."""
         import hashlib
+
+        def key(d):
+            # the sentence id; without one (a dataset that carries none), the
+            # element's own content: words, head locations and edge labels
+            i = d.get("id")
+            if i is not None:
+                return i
+            return tuple(tuple(d.get(k) or ()) for k in ("words_index", "words_head", "edges_index"))
         hsh = hashlib.blake2b(digest_size=8)
         for bidx, els in sched:
-            hsh.update(repr((bidx, [d.get("id") for d in els])).encode())
+            hsh.update(repr((bidx, [key(d) for d in els])).encode())
         dg = int.from_bytes(hsh.digest(), "little") >> 2
         dev = self.device if torch.distributed.get_backend(self.group) == "nccl" else torch.device("cpu")
         t = torch.tensor([dg, -dg], dtype=torch.int64, device=dev)

@@ -250,13 +250,15 @@ def test_explicit_backend_at_world_one_runs_the_collectives():
     assert q.get(timeout=5) == [True] * 6
 
 
-def _schedule_worker(rank, world, port, diverge, q):
+def _schedule_worker(rank, world, port, diverge, q, drop_ids=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as tdist
     from ggnn_amd.dist import init_from_env
     init_from_env(backend="gloo")
     m, data = _golden_model()
+    if drop_ids:           # a dataset without sentence ids: the digest keys on each element's content
+        data = [{k: x for k, x in d.items() if k != "id"} for d in data]
     m.rank, m.world_size = rank, world
     if diverge and rank == 1:
         np.random.seed(123)
@@ -270,8 +272,9 @@ def _schedule_worker(rank, world, port, diverge, q):
     tdist.destroy_process_group()
 
 
+@pytest.mark.parametrize("drop_ids", [False, True])
 @pytest.mark.parametrize("diverge", [False, True])
-def test_ranks_check_that_their_schedules_agree(diverge):
+def test_ranks_check_that_their_schedules_agree(diverge, drop_ids):
     """The model seeds the global RNGs as the reference does
     (chem_tensorflow.py:174-175), so ranks draw the same schedule; run_epoch
     compares a digest of it across the ranks once per epoch and raises when a
@@ -279,7 +282,7 @@ def test_ranks_check_that_their_schedules_agree(diverge):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_schedule_worker, args=(r, 2, port, diverge, q)) for r in range(2)]
+    procs = [ctx.Process(target=_schedule_worker, args=(r, 2, port, diverge, q, drop_ids)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -299,17 +299,23 @@ def _trees(b, v, E, seed, extra=0):
 
 
 def _run_edges(graphs, v, E, h0, w, T, precision="fp32", dhT=None, sparse="auto", dr=None, force_generic=False,
-               batch_pack=False):
+               batch_pack=False, skip=True):
     torch = _torch()
     from ggnn_amd.engine import PropagationEngine
     b, h = h0.shape[0], h0.shape[-1]
-    eng = PropagationEngine(h, 2 * E, precision=precision, sparse_pairs=sparse, force_generic=force_generic)
+    eng = PropagationEngine(h, 2 * E, precision=precision, sparse_pairs=sparse, force_generic=force_generic,
+                            skip_empty_channels=skip)
     dev = eng.device
     dr = dr or dict(edge_keep=1.0, state_keep=1.0, seed=0)
     wd = {k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in w.items()}
     if batch_pack:     # the model's order: stage the batch, then pack for it (ggnn_pack_weights_batch)
         eng.set_adjacency_edges(graphs, v, E)
-    pack = eng.pack_weights(wd, T=T, edge_keep=dr["edge_keep"], seed=dr["seed"], batch=batch_pack)
+    out = None
+    if batch_pack:     # every byte a NaN sentinel: a copy the pack skips must not be read
+        d = eng.dims(b, v, T, edge_keep=dr["edge_keep"], seed=dr["seed"])
+        from ggnn_amd import _lib
+        out = torch.full((_lib.weight_pack_bytes(d),), 0xFF, dtype=torch.uint8, device=dev)
+    pack = eng.pack_weights(wd, T=T, edge_keep=dr["edge_keep"], seed=dr["seed"], batch=batch_pack, out=out)
     if not batch_pack:
         eng.set_adjacency_edges(graphs, v, E)
     out = eng.forward(torch.from_numpy(np.ascontiguousarray(h0)).to(dev), pack, T, training=dhT is not None,
@@ -376,16 +382,23 @@ def test_sparse_pairs_dropout_fp32_parity(ek, sk, batch_pack):
         assert _nmax(got[k].reshape(gref[k].shape), gref[k]) <= FP32_TOL, k
 
 
-def test_batch_pack_masks_only_the_batch_channels():
+@pytest.mark.parametrize("mode", ["pairs", "tiles", "tiles_dense_channels"])
+def test_batch_pack_masks_only_the_batch_channels(mode):
     """ggnn_pack_weights_batch (the model's pack: stage, then pack for the
     batch): under edge dropout on the general path it writes the masked W_c
     copies only for channels with an edge in the staged batch -- a sentence
-    batch touches about half of the 92.  The step's results equal the full
-    pack's (h_T and dL/dh0 bit for bit; weight gradients up to the order of
-    their fp32 atomics), the skipped copies are left unwritten, and a pack made
-    for one staged batch is refused for the next."""
+    batch touches about half of the 92 -- in pair mode and on the dense-tile
+    general path; with GGNN_DENSE_CHANNELS (skip_empty_channels=False) every
+    tile runs, so it writes every copy.  The pack is made into a buffer of NaN
+    sentinels: the step's results equal the full pack's (h_T and dL/dh0 bit
+    for bit; weight gradients up to the order of their fp32 atomics), so no
+    skipped copy is read; the skipped copies still hold the sentinel; and a
+    pack made for one staged batch is refused for the next."""
     torch = _torch()
+    from ggnn_amd import _lib
     from ggnn_amd.engine import PropagationEngine
+    kw = {"pairs": dict(sparse="auto"), "tiles": dict(sparse=False, force_generic=True),
+          "tiles_dense_channels": dict(sparse=False, force_generic=True, skip=False)}[mode]
     b, v, h, T, E = 3, 30, 400, 3, 46
     graphs, A = _trees(b, v, E, seed=11)
     used = A.reshape(b, 2 * E, -1).max(axis=(0, 2)) > 0
@@ -395,20 +408,26 @@ def test_batch_pack_masks_only_the_batch_channels():
     w = O.synthetic_weights(h, 2 * E, seed=6)
     dhT = rng.standard_normal((b, v, h)).astype(np.float32)
     dr = dict(edge_keep=0.8, state_keep=0.9, seed=777)
-    full = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr)
-    part = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr, batch_pack=True)
+    full = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr, **kw)
+    part = _run_edges(graphs, v, E, h0, w, T, dhT=dhT, dr=dr, batch_pack=True, **kw)
+    assert part["sparse"] == (mode == "pairs")
     for k in ("hT", "h0"):
         assert np.array_equal(full[k], part[k]), k
     for k in GRADS[1:]:
-        assert _nmax(part[k], full[k]) <= 1e-6, k
+        assert np.isfinite(part[k]).all() and _nmax(part[k], full[k]) <= 1e-6, k
     # the copies: occupied channels masked exactly as the full pack, the others untouched
-    eng = PropagationEngine(h, 2 * E)
+    eng = PropagationEngine(h, 2 * E, sparse_pairs=kw["sparse"], force_generic=kw.get("force_generic", False),
+                            skip_empty_channels=kw.get("skip", True))
     wd = {k: torch.from_numpy(np.ascontiguousarray(x)).to(eng.device) for k, x in w.items()}
     eng.set_adjacency_edges(graphs, v, E)
+    nb = _lib.weight_pack_bytes(eng.dims(b, v, T, edge_keep=0.8, seed=777))
     pf = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777)
-    pb = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777, batch=True)
+    pb = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777, batch=True,
+                          out=torch.full((nb,), 0xFF, dtype=torch.uint8, device=eng.device))
     pb2 = eng.pack_weights(wd, T=T, edge_keep=0.8, seed=777, batch=True)
     torch.cuda.synchronize()
+    if mode == "tiles_dense_channels":
+        used = np.ones_like(used)
     al = lambda x: (x + 255) & ~255  # noqa: E731  (ggnn_api.hip pack_layout: beta, bg, bc, then the copies)
     C = 2 * E
     g_w = al(C * h * 4) + al(2 * h * 4) + al(h * 4)
@@ -419,6 +438,8 @@ def test_batch_pack_masks_only_the_batch_channels():
         cb = pb.buf[o:o + n].view(torch.float32).view(C, h * h)
         u = torch.from_numpy(used).to(eng.device)
         assert torch.equal(cf[u], cb[u]), t
+        raw = pb.buf[o:o + n].view(C, h * h * 4)
+        assert bool((raw[~u] == 0xFF).all()), t       # skipped copies: the sentinel, unwritten
     eng.set_adjacency_edges(graphs[:2], v, E)
     with pytest.raises(RuntimeError):
         eng.forward(torch.zeros((2, v, h), device=eng.device), pb2, T)
@@ -494,3 +515,36 @@ def test_pack_general_copies_vector_form_equals_scalar_form(h, keep):
         assert torch.equal(a, b), "timestep %d: vector and scalar copies differ" % t
     if keep == 1.0:
         assert torch.equal(pa.buf[g_w:g_w + n].view(torch.float32), w["edge_weights"].reshape(-1))
+
+
+@pytest.mark.parametrize("kernel", [3, 4, 5])
+@pytest.mark.parametrize("b_layout", [0, 1])
+def test_k_gemm_ks_limb_split_wait_states(kernel, b_layout):
+    """The inline-asm limb split (ggnn_common.h pk_lo: v_fma_mix{lo,hi}_f16)
+    feeds MFMA operands; its VALU -> MFMA wait states live inside the asm
+    string (round 4: without them k_gemm_ks read the previous fragment's lo
+    limbs).  Direct check on k_gemm_ks in fp32-parity mode: every A element is
+    1 + j * 2^-13 (hi limb 1, a distinct lo limb j * 2^-13 per element) and B is
+    one-hot, so each output is ONE A element, exact in fp32 only if its own
+    lo limb entered the product; a stale or missing lo limb shows as the exact
+    (m, n) it hits (tools/ks_debug.py / tools/limb_mix_test.hip)."""
+    M, N, K = 96, 64, 256
+    rng = np.random.default_rng(kernel * 2 + b_layout)
+    j = rng.integers(1, 64, (M, K))
+    A = (1.0 + j * 2.0 ** -13).astype(np.float32)
+    kk = rng.permutation(K)[:N]                           # output column n reads A[:, kk[n]]
+    B = np.zeros((K, N), np.float32)
+    B[kk, np.arange(N)] = 1.0
+    Bop = B if b_layout == 0 else np.ascontiguousarray(B.T)
+    got = _gemm_ex(A, 0, Bop, b_layout, M, N, K, "fp32", kernel)
+    want = A[:, kk]
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, (len(bad), bad[:5].tolist(), got[tuple(bad[0])], want[tuple(bad[0])])
+    # the same through the B side: A one-hot rows, B with distinct lo limbs
+    A2 = np.zeros((M, K), np.float32)
+    ka = rng.integers(0, K, M)
+    A2[np.arange(M), ka] = 1.0
+    B2 = (1.0 + rng.integers(1, 64, (K, N)) * 2.0 ** -13).astype(np.float32)
+    B2op = B2 if b_layout == 0 else np.ascontiguousarray(B2.T)
+    got2 = _gemm_ex(A2, 0, B2op, b_layout, M, N, K, "fp32", kernel)
+    assert np.array_equal(got2, B2[ka, :])

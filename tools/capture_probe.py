@@ -7,9 +7,9 @@ gradients (once a garbage pair index and a fault).  Run with
 
     GGNN_LIB=tools/libggnn_memset.so python tools/capture_probe.py
 
-where tools/libggnn_memset.so is ggnn_api.hip built with
--DGGNN_PROBE_MEMSET_NODES (fill_async / copy_async as hipMemsetAsync /
-hipMemcpyAsync, the round-2 form), to see whether every memset / memcpy node
+where tools/libggnn_memset.so (tools/build_memset_probe_lib.py) is libggnn
+with fill_async / copy_async as hipMemsetAsync / hipMemcpyAsync, the
+round-2 form, to see whether every memset / memcpy node
 is ordered after its producer and before its consumer; without GGNN_LIB it
 dumps the shipped kernel-only graph.  The step: the reference's default
 model at hidden 400 (general path, pair mode), T = 4, the training feed's

@@ -40,13 +40,16 @@ for k, cs in per.items():
         d["hbm_read_bytes_corrected"] = 2 * 1024 * d["FETCH_SIZE"]
     if "WRITE_SIZE" in d:
         d["hbm_write_bytes"] = 1024 * d["WRITE_SIZE"]
+    if d.get("TCC_HIT_sum") is not None and d.get("TCC_MISS_sum") is not None:
+        d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0)
     summary[k] = d
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1, sort_keys=True)
 for k in sorted(summary):
     d = summary[k]
     print("%-28s " % k[:28] + " ".join("%s=%.3g" % (c, d[c]) for c in (
         "frac_wait_any", "frac_wait_inst", "frac_active", "mfma_busy_per_busy_cycle", "SQ_LDS_BANK_CONFLICT",
-        "hbm_read_bytes_corrected", "hbm_write_bytes") if c in d))
+        "hbm_read_bytes_corrected", "hbm_write_bytes", "TCC_REQ_sum", "TCP_TCC_READ_REQ_sum", "l2_hit_rate")
+        if c in d))
 
 if len(sys.argv) > 2:
     kinds = {}

@@ -8,8 +8,11 @@
 set -e
 TAG=${1:-r02}
 export TMPDIR=/tmp
+# the bench's own timed leg and nothing else (dropout off, no side lines): the
+# k_fwd_fused / k_gru_bwd averages of this trace and the roofline of the JSON
+# line in ${TAG}_trace.log come from the same launches
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o bench -- \
-  python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --dropout-keep 1 > gpurun_out/${TAG}_trace.log 2>&1
+  python3 bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-side --no-dropout-leg > gpurun_out/${TAG}_trace.log 2>&1
 PMC_RUN=$TAG bash tools/pmc_profile.sh gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc.log 2>&1
 cp gpurun_out/${TAG}_pmc/pmc_traffic.json profiles/pmc_traffic.json
 PMC_RUN=$TAG bash tools/pmc_profile.sh gpurun_out/${TAG}_pmcbf16 --steps 2 --warmup 1 --no-cpu-baseline --no-side \
