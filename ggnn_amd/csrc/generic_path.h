@@ -21,7 +21,7 @@ struct GenAdjL {
   int vp;
   int nch, gch;  // cgc: every channel's graph list cut into nch chunks of <= gch graphs
   // pair mode (GGNN_SPARSE_PAIRS, k_pairs.h)
-  size_t degc, pidx, pcnt, poff, prow, pdeg, ptile, pmask, wtl, wmap, wmask;
+  size_t degc, pidx, pcnt, poff, prow, pdeg, ptile, pmask, wtl, wmap, wmask, wst;
   size_t rcnt, roff, rlist;  // reverse gather lists of the backward's dh scatter (k_pair_rev)
   int cap_tiles, zw;  // product tiles of the pair-row capacity; dW split-K chunks
 };
@@ -58,6 +58,7 @@ GenAdjL gen_adj_layout(const Cfg& c) {
     L.wtl = o;   o += al((size_t)L.zw * (1 + PAIR_CHUNK) * 4);
     L.wmap = o;  o += al((size_t)L.zw * 4);
     L.wmask = o; o += al((size_t)L.zw);
+    L.wst = o;   o += al((size_t)(c.C + 1) * 4);  // channel c's dW chunks: z in [wst[c], wst[c+1])
     L.rcnt = o;  o += al(N * 4);
     L.roff = o;  o += al((N + 1) * 4);
     L.rlist = o; o += al((size_t)c.pcap * 4);
@@ -74,6 +75,11 @@ struct GenWsL {
   // the timestep loop; WTL: its term lists, every timestep's tiles of a chunk)
   size_t WTL, pslice;
   size_t MB;  // edge-dropout keep bits of every timestep (k_edge_bits; pair mode, training)
+  // deterministic reductions (round 5): split-K slabs of the weight-gradient
+  // products (GemmArgs::slab), the element-wise kernels' bias partials
+  // [T][slices][dbg_r | dbg_u | dbc], pair mode's per-tile dbeta partials
+  // [T][cap_tiles][H], and k_sum_rows' chunk sums
+  size_t SLAB, GBP, PDB, SUMS, CSP;  // CSP: the dense tiles' dbeta column-sum partials [b][C][v/32][H]
   size_t py(int t) const { return PY + (size_t)t * pslice * 4; }
   size_t pdx(int t) const { return PDX + (size_t)t * pslice * 4; }
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
@@ -87,6 +93,51 @@ struct GenWsL {
   size_t rh(int t) const { return RH + (size_t)(t % ns) * nh * 4; }
   size_t cc(int t) const { return CC + (size_t)(t % ns) * nh * 4; }
 };
+// rows per slice of the element-wise backward kernels (k_gen_bwd1 / 2): >= 8
+// rows each, at most 1024 slices; one bias partial row per slice
+long gen_bias_slices(const Cfg& c) {
+  const long N = (long)c.b * c.vin;
+  return std::max<long>(1, std::min<long>(1024, (N + 7) / 8));
+}
+// split-K plan of one GRU weight-gradient product with Nn output columns:
+// large batches: z = a chunk of rows, the T timesteps as its terms (~512
+// workgroups); small: z = (chunk, timestep), ~1024 workgroups
+struct GenWgPlan {
+  long KC;
+  int Z, nterm, zdiv;
+};
+GenWgPlan gen_wg_plan(const Cfg& c, long Nn) {
+  const long N = (long)c.b * c.vin, H = c.H;
+  const long tiles = ((H + 127) / 128) * ((Nn + 127) / 128);
+  GenWgPlan p;
+  if (N / 128 >= 512 / tiles) {
+    const long want = std::max<long>(1, 512 / tiles);
+    p.KC = std::min<long>(((N + want - 1) / want + 31) & ~31L, (N + 31) & ~31L);
+    p.nterm = c.T;
+    p.zdiv = 1;
+    p.Z = (int)((N + p.KC - 1) / p.KC);
+  } else {
+    const long zt = std::max<long>(1, 1024 / tiles);
+    long KC = ((c.T * N + zt - 1) / zt + 31) & ~31L;
+    p.KC = std::min<long>(std::max<long>(KC, 256), (N + 31) & ~31L);
+    p.nterm = 0;
+    p.zdiv = c.T;
+    p.Z = (int)((N + p.KC - 1) / p.KC) * c.T;
+  }
+  return p;
+}
+GenAdjL gen_adj_layout(const Cfg& c);
+// floats of the largest split-K slab one backward needs
+size_t gen_slab_floats(const Cfg& c) {
+  const size_t H = c.H;
+  size_t m = 0;
+  for (long Nn : {(long)H, 2 * (long)H}) m = std::max(m, (size_t)gen_wg_plan(c, Nn).Z * H * Nn);
+  const GenAdjL AL = gen_adj_layout(c);
+  if (c.sparse) m = std::max(m, (size_t)AL.zw * H * H);
+  else if (AL.nch > 1) m = std::max(m, (size_t)c.C * AL.nch * H * H);
+  return m;
+}
+
 GenWsL gen_ws_layout(const Cfg& c, bool tr) {
   GenWsL L;
   memset(&L, 0, sizeof(L));
@@ -124,6 +175,11 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
     L.DRH = o; o += a4;
     if (c.ed && !c.sparse) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
     L.gmax = o; o += al(4);
+    L.SLAB = o; o += al(gen_slab_floats(c) * 4);
+    L.GBP = o;  o += al((size_t)c.T * gen_bias_slices(c) * 3 * H * 4);
+    if (c.sparse) { L.PDB = o; o += al((size_t)c.T * (c.pcap / PAIR_TILE) * H * 4); }
+    L.SUMS = o; o += al((size_t)SUM_RCS * (3 * H + c.C * H) * 4);
+    if (!c.sparse) { L.CSP = o; o += al((size_t)c.b * c.C * ((c.vin + 31) / 32) * H * 4); }
   }
   L.total = o;
   return L;
@@ -320,7 +376,7 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
                        P<int>(adj, L.pidx), P<int>(adj, L.pcnt));
     hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
                        P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
-                       P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask));
+                       P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask), P<int>(adj, L.wst));
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
                        P<int>(adj, L.prow), P<float>(adj, L.pdeg));
@@ -513,11 +569,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // (row slices of the element-wise kernels: >= 8 rows each, at most 1024 slices; one bias
     // atomic per column per slice.  A small batch -- 20 sentences, N ~ 560 rows -- needs the
     // short slices: a thread walks its slice's rows one after another)
-    const dim3 ewg((unsigned)((H + 255) / 256), (unsigned)std::max<long>(1, std::min<long>(1024, (N + 7) / 8)));
+    const dim3 ewg((unsigned)((H + 255) / 256), (unsigned)gen_bias_slices(c));
+    float* gbp = P<float>(ws, L.GBP) + (size_t)t * ewg.y * 3 * H;  // this timestep's bias partial rows
     {
       Prof p(K_GRU_BWD, s);
       hipLaunchKernelGGL(k_gen_bwd1, ewg, dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)), DZC, DZG, DXH, N,
-                         c.H, dbc, dbg);
+                         c.H, gbp);
     }
     // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k]), one launch
     // over both halves: columns n >= H go to d(rh) (a separate [N][H] buffer)
@@ -532,7 +589,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     }
     {
       Prof p(K_GRU_BWD, s);
-      hipLaunchKernelGGL(k_gen_bwd2, ewg, dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H, dbg);
+      hipLaunchKernelGGL(k_gen_bwd2, ewg, dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H, gbp);
     }
     // [dX | dh] += dzg Wg^T
     {
@@ -557,12 +614,11 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
                            AL.cap_tiles * PAIR_TILE,
                            c.H);
         if (use_bias)
-          // (row slices of >= 16 rows; up to N / 32 of them: a channel may hold every node row)
-          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)C,
-                                                (unsigned)std::min<long>(256, std::max<long>(8, (N + 31) / 32))),
-                             dim3(256), 0, s,
-                             P<const int>(adj, AL.poff), P<const int>(adj, AL.pcnt), P<const float>(adj, AL.pdeg), PDX,
-                             dbeta, c.H);
+          // per pair tile (one channel's rows): sum of deg * dXg, summed per
+          // channel in tile order after the timestep loop
+          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)AL.cap_tiles), dim3(256), 0, s,
+                             P<const unsigned char>(adj, AL.pmask), P<const float>(adj, AL.pdeg), PDX,
+                             P<float>(ws, L.PDB) + (size_t)t * AL.cap_tiles * H, c.H);
       }
       if (int e = gen_pairs_product<PREC>(c, AL, adj, PDX, P<float>(pack, PL.gw(c.ed ? t : 0)), true, PZ, K_PROP_BWD,
                                           s))
@@ -582,9 +638,19 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.D = dM; a.sDz = v * H; a.sDm = H; a.sDn = 1;
       a.zdiv = (int)C; a.Z = (int)(c.b * C); a.zmask = dense_ch ? nullptr : P<unsigned char>(adj, AL.occ);
       a.M = (int)v; a.N = (int)H; a.K = (int)v;
-      // dbeta_c += column sums of dM[g,c] (the edge bias enters every message row)
-      if (use_bias) { a.csum = dbeta; a.scq = H; }
+      // dbeta_c += column sums of dM[g,c] (the edge bias enters every message
+      // row): per (graph, channel, 32-row slice) partials, summed in a fixed
+      // order below (deterministic)
+      if (use_bias) { a.csum = dbeta; a.scq = H; a.cpart = P<float>(ws, L.CSP); a.cslots = (int)((v + 31) / 32); }
       if (int e = gg_launch<PREC>(a, true, true, false, K_PROP_BWD, s)) return e;
+      if (use_bias) {
+        Prof p(K_PROP_BWD, s);
+        SumPlan sp(P<float>(ws, L.SUMS));
+        const long S = a.cslots;
+        SumJob& q = sp.add(a.cpart, (int)c.b, (int)S, C * S * H, H, C * H, H, S * H, dbeta, dbeta, C * H, 1);
+        if (!dense_ch) { q.mask = P<const unsigned char>(adj, AL.occ); q.mT = C; q.mC = 1; }
+        sp.launch(s);
+      }
     }
     // dh[g] += sum over g's channels of dM[g,c] W_c^T
     {
@@ -600,7 +666,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     {
       float* G_out = c.ed ? P<float>(ws, L.GW) : dW;
       const bool chunked = AL.nch > 1;
-      if (chunked && c.ed) fill_async(G_out, 0, (size_t)C * H * H * 4, s);
       GemmArgs a = gg_args();
       a.A = ht; a.sAq = v * H; a.sAm = 1; a.sAk = H;
       a.B = dM; a.sBp = v * H; a.sBq = C * v * H; a.sBk = H; a.sBn = 1;
@@ -608,8 +673,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.mode = chunked ? GG_ATOMIC : c.ed ? GG_STORE : GG_ADD;
       a.tl = P<int>(adj, AL.cgc); a.ts = AL.gch + 1; a.zdiv = AL.nch;  // z = (channel, chunk of its graphs)
       a.Z = (int)C * AL.nch; a.M = (int)H; a.N = (int)H; a.K = (int)v;
+      // chunks of one channel: slab partials, summed in chunk order (added
+      // into dW over the timesteps; stored into this timestep's GW under edge dropout)
+      if (chunked) { a.slab = P<float>(ws, L.SLAB); a.sSlab = H * H; }
       if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
+      if (chunked) slab_reduce(a, (int)C, AL.nch, nullptr, 0, c.ed ? 0 : 1, H * H, s);
       if (c.ed)
         hipLaunchKernelGGL(k_gen_wmask_acc, dim3(grid1d(C * ((H + 3) / 4) * H)), dim3(256), 0, s, P<const float>(ws, L.GW), dW,
                            c.C, c.H, t, c.edrop);
@@ -641,6 +710,9 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     a.tl = P<const int>(ws, L.WTL); a.ts = 1 + (long)c.T * PAIR_CHUNK;
     a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
     a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
+    // a channel's only chunk stores its dW (zmask 2); several chunks: slab
+    // partials summed in chunk order (k_slab_reduce, below)
+    a.slab = P<float>(ws, L.SLAB); a.sSlab = H * H;
     if (c.ed) {
       a.dr = c.edrop; a.tgroups = c.T;
       // the masks as bits, drawn once per (channel with pairs, timestep, weight)
@@ -655,6 +727,8 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.mbits = mb; a.mbw = w32; a.mbC = (int)C;
     }
     if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
+    Prof p(K_WGRAD, s);
+    slab_reduce(a, (int)C, 0, P<const int>(adj, AL.wst), 1, 0, H * H, s);
   }
   // GRU weight gradients over all T*N rows at once, split-K with fp32
   // atomics, which bound these products at ~65 G adds/s.  Large batches: z =
@@ -666,31 +740,40 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   // which measured faster there (20 sentences: 0.303 vs 0.336 ms)
   {
     auto wg = [&](size_t aoff, long slotA, size_t boff, long ldB, long slotB, int Nn, float* out, long ldO) {
-      const long tiles = ((H + 127) / 128) * ((Nn + 127) / 128);
+      const GenWgPlan pl = gen_wg_plan(c, Nn);
       GemmArgs a = gg_args();
       a.A = P<float>(ws, aoff); a.sAq = slotA; a.sAm = 1; a.sAk = H;
       a.B = P<float>(ws, boff); a.sBq = slotB; a.sBk = ldB; a.sBn = 1;
       a.D = out; a.sDm = ldO; a.sDn = 1; a.mode = GG_ATOMIC;
       a.M = (int)H; a.N = Nn; a.Ktot = N;
-      long KC;
-      if (N / 128 >= 512 / tiles) {
-        const long want = std::max<long>(1, 512 / tiles);
-        KC = std::min<long>(((N + want - 1) / want + 31) & ~31L, (N + 31) & ~31L);
-        a.nterm = c.T; a.Z = (int)((N + KC - 1) / KC);
-      } else {
-        const long zt = std::max<long>(1, 1024 / tiles);
-        KC = ((c.T * N + zt - 1) / zt + 31) & ~31L;
-        KC = std::min<long>(std::max<long>(KC, 256), (N + 31) & ~31L);
-        a.zdiv = c.T; a.Z = (int)((N + KC - 1) / KC) * c.T;
-      }
-      a.sAp = KC * H; a.sBp = KC * ldB; a.K = (int)KC; a.sKp = KC;
-      return gg_launch<WPREC>(a, false, false, false, K_WGRAD, s);
+      a.nterm = pl.nterm; a.zdiv = pl.zdiv; a.Z = pl.Z;
+      a.sAp = pl.KC * H; a.sBp = pl.KC * ldB; a.K = (int)pl.KC; a.sKp = pl.KC;
+      // the z partials in a slab, summed in z order (deterministic)
+      a.slab = P<float>(ws, L.SLAB); a.sSlab = H * Nn;
+      if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
+      Prof p(K_WGRAD, s);
+      slab_reduce(a, 1, a.Z, nullptr, 0, 0, 0, s);
+      return (int)GGNN_OK;
     };
     const long sl = (long)L.nh;  // floats between timestep slots of an [N][H] array
     if (int e = wg(L.x(0), sl, L.dzc(0), H, sl, (int)H, dWc, H)) return e;
     if (int e = wg(L.rh(0), sl, L.dzc(0), H, sl, (int)H, dWc + H * H, H)) return e;
     if (int e = wg(L.x(0), sl, L.dzg(0), 2 * H, 2 * sl, (int)(2 * H), dWg, 2 * H)) return e;
     if (int e = wg(L.hsl(0), sl, L.dzg(0), 2 * H, 2 * sl, (int)(2 * H), dWg + H * 2 * H, 2 * H)) return e;
+  }
+  {
+    Prof p(K_IO, s);
+    // bias gradients: fixed-order sums of the per-(timestep, slice) GRU bias
+    // rows and of pair mode's per-(timestep, tile) dbeta partials
+    SumPlan sp(P<float>(ws, L.SUMS));
+    const int nsl = (int)gen_bias_slices(c);
+    sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H);
+    sp.launch(s);
+    if (c.sparse && use_bias) {
+      GemmArgs r = gg_args();
+      r.slab = P<float>(ws, L.PDB); r.sSlab = H; r.D = dbeta; r.sDm = 0; r.M = 1; r.N = (int)H;
+      slab_reduce_t(r, (int)C, P<const int>(adj, AL.poff), PAIR_TILE, c.T, AL.cap_tiles, s);
+    }
   }
   {
     Prof p(K_IO, s);

@@ -220,10 +220,95 @@ AdjL adj_layout(const Cfg& c) {
 struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
-  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp, gmax;
+  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp, gmax, wpart, gbp, sump;
   size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
+// the weight-gradient launch's plan (k_wgrad / k_wgrad256): output tile size,
+// K chunk, tiles (incl. the per-timestep dW tiles under edge dropout) and the
+// tiles of T-summed problems the chunk count is sized by
+struct WgPlan {
+  int TS;
+  long KC, nchunks, tiles, tiles_eq;
+};
+long wg256_kc(const Cfg& c);
+WgPlan wg_plan(const Cfg& c) {
+  WgPlan w;
+  const long N = c.N, H = c.H;
+  const bool big = H == 256 && N % 128 == 0;
+  w.TS = big ? 256 : 128;
+  const long t2 = (H / w.TS) * (H / w.TS);
+  w.tiles_eq = (6 + c.C) * t2;
+  w.tiles = (6 + (c.ed ? (long)c.T * c.C : c.C)) * t2;
+  if (big) {
+    w.KC = wg256_kc(c);
+  } else {
+    long KC = 4096;
+    while (KC > 32 && (N % KC) != 0) KC /= 2;
+    while (KC > 256 && w.tiles_eq * (N / KC) < 256) KC /= 2;
+    w.KC = KC;
+  }
+  w.nchunks = std::max<long>(N / std::max<long>(w.KC, 1), 1);
+  return w;
+}
+// rows of k_gru_bwd's per-workgroup bias partials (one row per (timestep, workgroup))
+long gru_bias_rows(const Cfg& c);
+constexpr int SUM_RCS = 32;  // k_sum_rows' row chunks (at most)
+// Builder of one k_sum_rows / k_sum_rows_fin pair (fixed-order column sums):
+// jobs take consecutive pieces of the scratch at `scr` (SUM_RCS * E floats
+// each at most)
+struct SumPlan {
+  SumJobs sj;
+  int nb = 0, nf = 0;
+  float* scr;
+  explicit SumPlan(float* scratch) : scr(scratch) { memset(&sj, 0, sizeof(sj)); }
+  // rows (t, w): part + t * sT + w * sW + (e / Nc) * sC + e % Nc
+  SumJob& add(const float* part, int T, int nw, long sT, long sW, long E, long Nc, long sC, float* o0, float* o1,
+              long split, int accumulate = 0) {
+    SumJob& q = sj.j[sj.count];
+    const long rows = (long)T * nw;
+    q.part = part; q.T = T; q.nw = nw; q.sT = sT; q.sW = sW; q.E = E; q.Nc = Nc; q.sC = sC;
+    q.split = split; q.out0 = o0; q.out1 = o1; q.add = accumulate;
+    q.rcs = (int)std::max<long>(1, std::min<long>(SUM_RCS, rows / 16));
+    q.scratch = scr;
+    scr += (long)q.rcs * E;
+    sj.bx[sj.count] = nb;
+    sj.fx[sj.count++] = nf;
+    nb += (int)((E + 63) / 64) * q.rcs;
+    nf += (int)((E + 255) / 256);
+    return q;
+  }
+  // rows of E contiguous columns, row (t, w) at part + (t * stride + w) * E
+  SumJob& rows(const float* part, int T, int nw, long stride, long E, float* o0, float* o1, long split) {
+    return add(part, T, nw, stride * E, E, E, E, 0, o0, o1, split);
+  }
+  void launch(hipStream_t s) {
+    if (!sj.count) return;
+    sj.bx[sj.count] = nb;
+    sj.fx[sj.count] = nf;
+    hipLaunchKernelGGL(k_sum_rows, dim3(nb), dim3(256), 0, s, sj);
+    hipLaunchKernelGGL(k_sum_rows_fin, dim3(nf), dim3(256), 0, s, sj);
+  }
+};
+// k_slab_reduce over groups of z (GemmArgs::slab)
+void slab_reduce(const GemmArgs& a, int G, int zper, const int* zs, int sole, int add, long sDg, hipStream_t s) {
+  SlabRed r;
+  memset(&r, 0, sizeof(r));
+  r.slab = a.slab; r.sSlab = a.sSlab; r.D = a.D; r.sDg = sDg; r.sDm = a.sDm;
+  r.M = a.M; r.N = a.N; r.G = G; r.zper = zper; r.zs = zs; r.zsdiv = 1; r.nt = 1; r.zmask = a.zmask;
+  r.sole = sole; r.add = add;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256), (unsigned)G), dim3(256), 0, s, r);
+}
+// the same over nt per-timestep slab sets of zT z's each, group g's z in
+// [zs[g] / zsdiv, zs[g+1] / zsdiv) (stored, not added)
+void slab_reduce_t(const GemmArgs& a, int G, const int* zs, int zsdiv, int nt, long zT, hipStream_t s) {
+  SlabRed r;
+  memset(&r, 0, sizeof(r));
+  r.slab = a.slab; r.sSlab = a.sSlab; r.zT = zT; r.D = a.D; r.sDg = (long)a.M * a.N; r.sDm = a.sDm;
+  r.M = a.M; r.N = a.N; r.G = G; r.zs = zs; r.zsdiv = zsdiv; r.nt = nt;
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256), (unsigned)G), dim3(256), 0, s, r);
+}
+
 WsL ws_layout(const Cfg& c, bool training) {
   WsL L;
   memset(&L, 0, sizeof(L));
@@ -258,6 +343,12 @@ WsL ws_layout(const Cfg& c, bool training) {
     if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
     L.dbp = o; o += al(T * (size_t)c.b * C * H * 4);    // per-(timestep, graph) dL/dbeta partials
     L.gmax = o; o += al(4);                               // max |dL/dh_T| (gradient scale, ggnn_common.h)
+    if (H >= 128) {                                       // deterministic K-chunk reduction of the weight gradients
+      const WgPlan w = wg_plan(c);
+      L.wpart = o; o += al((size_t)w.tiles * w.nchunks * w.TS * w.TS * 4);
+    }
+    L.gbp = o; o += al((size_t)gru_bias_rows(c) * 3 * H * 4);  // k_gru_bwd's [dbg | dbc] partials
+    L.sump = o; o += al((size_t)SUM_RCS * (3 * H + C * H) * 4);  // k_sum_rows' per-row-chunk sums
   }
   L.total = o;
   return L;
@@ -375,12 +466,14 @@ void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const fl
 template <int H, int RT, int PREC>
 void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
                     const PackL& PL, const void* pk, void* dXT, float* dh_out, void* dzcT, void* dzgT, float* dbc,
-                    float* dbg, const uint32_t* gmax, hipStream_t s) {
+                    float* dbg, const uint32_t* gmax, float* bpart, int* nwg, hipStream_t s) {
   Prof p(K_GRU_BWD, s);
+  *nwg = (int)(c.N / (32 * RT));
   hipLaunchKernelGGL((k_gru_bwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, delta, hf, r, u, cc,
                      P<u16>(pk, PL.WcT), P<u16>(pk, PL.WgT), PL.loWc, PL.loWg, (ActT<PREC>*)dXT, dh_out,
-                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N, gmax);
+                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N, gmax, bpart);
 }
+long gru_bias_rows(const Cfg& c) { return (long)c.T * std::max<long>(c.N / 32, 1); }
 
 #define DISPATCH_V(c, FN, H, PREC, ...)                 \
   do {                                                  \
@@ -564,15 +657,10 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
 
   {
+    // (the weight and bias gradients need no clearing: k_wgrad_reduce,
+    // k_edge_mask_reduce and k_sum_rows store every element once)
     Prof p(K_IO, s);
     Zeroer z(s);
-    z.add(dW, (long)c.C * H * H);
-    z.add(dWg, 4 * H * H);
-    z.add(dbg, 2 * H);
-    z.add(dWc, 2 * H * H);
-    z.add(dbc, H);
-    if (c.ed) z.add(P<float>(ws, L.G), (long)c.T * c.C * H * H);
-    if (use_bias) z.add(dbeta, (long)c.C * H);
     z.add(P<float>(ws, L.gmax), 1);
   }
   // gradient scale: the backward runs on S * dL/dh_T, S = 2^-floor(log2 max|dL/dh_T|),
@@ -595,6 +683,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N / 4 * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
                        c.sdrop, c.T - 1, gmax);
   }
+  const long gb_stride = std::max<long>(N / 32, 1);  // bias-partial rows per timestep (k_gru_bwd, RT = 1 bound)
+  int gb_nwg = 0;
   for (int t = c.T - 1; t >= 0; --t) {
     const bool first = t == c.T - 1 && in_place, last = t == 0 && dense;
     const float* delta = first ? dhT : dA;
@@ -602,7 +692,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     DISPATCH_HRT(c, launch_gru_bwd, PREC, c, delta, P<float>(ws, L.hfT + L.nh4 * t), P<float>(ws, L.r + L.nh4 * t),
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg,
-                 first ? gmax : (const uint32_t*)nullptr, s);
+                 first ? gmax : (const uint32_t*)nullptr, P<float>(ws, L.gbp) + (size_t)t * gb_stride * 3 * H,
+                 &gb_nwg, s);
     DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg),
                 chan_lists(c, adj, AL), PL, pack,
                 dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t),
@@ -623,9 +714,12 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     if (!dense)
       hipLaunchKernelGGL(k_unpad_state, dim3(grid1d((long)c.b * c.vin * H)), dim3(256), 0, s, dA, c.vin, c.V, c.H, dh0,
                          (long)c.b, gmax);
-    if (use_bias)
-      hipLaunchKernelGGL(k_sum_graphs, dim3(grid1d((long)c.C * H, 64), 64), dim3(64), 0, s, P<const float>(ws, L.dbp),
-                         dbeta, c.T * c.b, (long)c.C * H);
+    // bias gradients: fixed-order sums of the per-(timestep, graph) dbeta and
+    // the per-(timestep, workgroup) GRU bias partials
+    SumPlan sp(P<float>(ws, L.sump));
+    sp.rows(P<const float>(ws, L.gbp), c.T, gb_nwg, gb_stride, 3 * H, dbg, dbc, 2 * H);
+    if (use_bias) sp.rows(P<const float>(ws, L.dbp), 1, c.T * c.b, c.T * c.b, (long)c.C * H, dbeta, dbeta, (long)c.C * H);
+    sp.launch(s);
     // weight gradients / S
     ZeroJobs j;
     memset(&j, 0, sizeof(j));
@@ -697,8 +791,14 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   // GRU-gradient workgroups (all nt timesteps each), which then set the launch
   // time (measured +0.27 ms per step at config 3 with keep 0.9)
   const long tiles_eq = c.ed ? tiles - (long)(nt - 1) * c.C * a.p[np - 1].tiles_b : tiles;
+  const WgPlan wp = wg_plan(c);
+  if (wp.tiles_eq != tiles_eq || wp.tiles < tiles || wp.TS != TS)
+    return fail(GGNN_EINVAL, "weight gradients: launch plan and workspace disagree");
+  // deterministic reduction over the K chunks (k_wgrad_reduce): the partial
+  // tiles live in the workspace
+  a.part = P<float>(ws, L.wpart);
   if (big) {
-    const long KC = wg256_kc(c);
+    const long KC = wp.KC;
     if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
     if (tiles_eq != 6 + c.C) return fail(GGNN_EINVAL, "k_wgrad256: unexpected problem set");
     a.KC = (int)KC;
@@ -713,11 +813,10 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
     }
     Prof p(K_WGRAD, s);
     hipLaunchKernelGGL((k_wgrad256<WP>), dim3(tiles * a.nchunks), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(k_wgrad_reduce<256>, dim3(tiles * 64), dim3(256), 0, s, a);
     return GGNN_OK;
   }
-  int KC = 4096;
-  while (KC > 32 && (N % KC) != 0) KC /= 2;
-  while (KC > 256 && tiles_eq * (N / KC) < 256) KC /= 2;
+  const int KC = (int)wp.KC;
   if (N % KC) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
   a.KC = KC;
   a.nchunks = (int)(N / KC);
@@ -726,6 +825,7 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
     Prof p(K_WGRAD, s);
     if (KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, WP>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_wgrad<64, WP>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_wgrad_reduce<128>, dim3(tiles * 16), dim3(256), 0, s, a);
   }
   LAUNCHCHK();
   return GGNN_OK;
@@ -1253,6 +1353,80 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
   return GGNN_OK;
 }
 
+// ---- deterministic embedding backward (fixed-point accumulation, k_head.h)
+namespace {
+struct EmbWsL {
+  size_t acc[GGNN_EMBED_MAX_SEGMENTS], own[GGNN_EMBED_MAX_SEGMENTS], sqp, total;
+};
+// one accumulator and owner-slot region per segment (segments sharing a
+// d_table use the first one's at call time)
+int emb_ws_layout(const ggnn_embed_segment* segs, int nseg, EmbWsL* L, const char* what) {
+  if (!segs || nseg < 1 || nseg > GGNN_EMBED_MAX_SEGMENTS)
+    return fail(GGNN_EINVAL, std::string(what) + ": 1.." + std::to_string(GGNN_EMBED_MAX_SEGMENTS) + " segments");
+  size_t o = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].rows < 1 || segs[i].width < 1) return fail(GGNN_EINVAL, std::string(what) + ": bad segment");
+    L->acc[i] = o; o += al((size_t)segs[i].rows * segs[i].width * 8);
+    L->own[i] = o; o += al((size_t)segs[i].rows * 4);
+  }
+  L->sqp = o; o += al((size_t)EMB_SQ_BLOCKS * EMB_MAXSEG * 4);
+  L->total = o;
+  return GGNN_OK;
+}
+}  // namespace
+
+int ggnn_embed_workspace_bytes(const ggnn_embed_segment* segs, int nseg, size_t* bytes) {
+  EmbWsL L;
+  if (int e = emb_ws_layout(segs, nseg, &L, "embed_workspace_bytes")) return e;
+  if (!bytes) return fail(GGNN_EINVAL, "embed_workspace_bytes: NULL pointer");
+  *bytes = L.total;
+  return GGNN_OK;
+}
+
+int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, const int32_t* word_inputs,
+                           int ncols, float keep, uint64_t seed, const float* dh0, const float* dh0_add,
+                           float* lookup_sqnorm, void* ws, ggnn_stream_t stream) {
+  EmbArgs a;
+  if (int e = emb_args(d, segs, nseg, ncols, keep, seed, &a, "embed_backward_ws")) return e;
+  EmbWsL L;
+  if (int e = emb_ws_layout(segs, nseg, &L, "embed_backward_ws")) return e;
+  if (!word_inputs || !dh0 || !lookup_sqnorm || !ws) return fail(GGNN_EINVAL, "embed_backward_ws: NULL pointer");
+  EmbGrad gd;
+  EmbAcc ea;
+  memset(&gd, 0, sizeof(gd));
+  memset(&ea, 0, sizeof(ea));
+  for (int i = 0; i < nseg; ++i) {
+    if (!segs[i].d_table) return fail(GGNN_EINVAL, "embed_backward_ws: NULL d_table");
+    gd.dtable[i] = segs[i].d_table;
+    // segments sharing a d_table (btb: the loc table, word_inputs columns 0
+    // and 3) accumulate in the first one's region; its squared norm slot too
+    int u = i;
+    for (int j = 0; j < i; ++j)
+      if (segs[j].d_table == segs[i].d_table) { u = j; break; }
+    if (segs[u].rows != segs[i].rows || segs[u].width != segs[i].width)
+      return fail(GGNN_EINVAL, "embed_backward_ws: segments sharing a d_table disagree on its shape");
+    gd.sqslot[i] = u;
+    ea.acc[i] = P<long long>(ws, L.acc[u]);
+    ea.own[i] = P<int>(ws, L.own[u]);
+  }
+  if (a.rows * nseg > 0x7fffffffL / 64 || a.rows >= (1L << 27))
+    return fail(GGNN_EINVAL, "embed_backward_ws: too many lookup rows");
+  hipStream_t s = (hipStream_t)stream;
+  Prof p(K_HEADS, s);
+  {
+    Zeroer z(s);
+    for (int i = 0; i < nseg; ++i) z.add(segs[i].d_table, (long)segs[i].rows * segs[i].width);
+  }
+  const int nblk = std::min(grid1d((a.rows + 3) / 4 * a.H), EMB_SQ_BLOCKS);
+  float* sqp = P<float>(ws, L.sqp);
+  hipLaunchKernelGGL(k_embed_bwd_det, dim3(nblk), dim3(256), 0, s, a, ea, word_inputs, dh0, dh0_add, sqp);
+  const long waves = a.rows * nseg;
+  hipLaunchKernelGGL(k_embed_fin, dim3((unsigned)((waves + 3) / 4 + 1)), dim3(256), 0, s, a, ea, gd, word_inputs, sqp,
+                     nblk, lookup_sqnorm);
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
 namespace {
 // All heads side by side: head i owns columns [off[i], off[i] + o_i) of the
 // concatenated operands (width Ot, each head padded to a multiple of 4 with
@@ -1262,8 +1436,11 @@ namespace {
 constexpr int HEAD_LP = 2048;  // loss partials per head (one per softmax block)
 struct HeadL {
   int off[GGNN_MAX_HEADS], Ot;
-  size_t W, Sx, bias, Z, dZ, dW, lp, total;
+  size_t W, Sx, bias, Z, dZ, dW, lp, slab, dbp, sums, total;
 };
+// the heads' dW product: split-K over node rows, chunks of KC rows
+long head_dw_kc(long rows) { return std::max<long>(256, ((rows + 47) / 48 + 31) & ~31L); }
+constexpr int HEAD_DZ_BLOCKS = 256;  // k_head_dz blocks (at most): one bias partial row each
 int head_layout(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, HeadL* L, const char* what) {
   if (int e = plain_dims(d, what)) return e;
   if (!heads || nheads < 1 || nheads > GGNN_MAX_HEADS)
@@ -1285,6 +1462,12 @@ int head_layout(const ggnn_dims* d, const ggnn_output_head* heads, int nheads, H
   L->dZ = o;   o += al(rows * Ot * 4);
   L->dW = o;   o += al(K * Ot * 4);
   L->lp = o;   o += al((size_t)nheads * HEAD_LP * 4);
+  // deterministic reductions: the dW product's split-K slab, the bias
+  // partials of k_head_dz (one row per block) and k_sum_rows' chunk sums
+  const long kc = head_dw_kc((long)rows);
+  L->slab = o; o += al((size_t)((rows + kc - 1) / kc) * K * Ot * 4);
+  L->dbp = o;  o += al((size_t)HEAD_DZ_BLOCKS * Ot * 4);
+  L->sums = o; o += al((size_t)SUM_RCS * Ot * 4);
   L->total = o;
   return GGNN_OK;
 }
@@ -1378,24 +1561,25 @@ static int heads_backward_impl(const ggnn_dims* d, const ggnn_output_head* heads
   Prof p(K_HEADS, s);
   float* dZ = P<float>(ws, L.dZ);
   float* dW = P<float>(ws, L.dW);
-  {
-    Zeroer z(s);
-    for (int i = 0; i < nheads; ++i) z.add(heads[i].d_bias, heads[i].o);
-    z.add(dW, (long)K * Ot);
-  }
+  float* dbp = P<float>(ws, L.dbp);
+  // (every bias and dW element is stored once by the fixed-order sums below)
+  const int nbz = (int)std::min<long>(HEAD_DZ_BLOCKS, (rows + 15) / 16);
+  SumPlan sp(P<float>(ws, L.sums));
   for (int i = 0; i < nheads; ++i) {
     const ggnn_output_head& hd = heads[i];
     const int o = hd.o, op = (o + 3) & ~3;
-    const dim3 g((unsigned)std::min<long>(256, (rows + 15) / 16));  // (bias atomics: one per column per block)
+    // bias: one column-partial row per block (dbp[block][off + j]), summed in block order
 #define HDZ(NI_)                                                                                                  \
-  hipLaunchKernelGGL(k_head_dz<NI_>, g, dim3(256), 0, s, hd.probs, hd.labels, rows, o, op,                       \
-                     tn_dev ? 1.0f : 1.0f / target_num, tn_dev, d_loss, dZ + L.off[i], Ot, hd.d_bias)
+  hipLaunchKernelGGL(k_head_dz<NI_>, dim3((unsigned)nbz), dim3(256), 0, s, hd.probs, hd.labels, rows, o, op,    \
+                     tn_dev ? 1.0f : 1.0f / target_num, tn_dev, d_loss, dZ + L.off[i], Ot, dbp + L.off[i], Ot)
     if (op <= 64) HDZ(1);
     else if (op <= 128) HDZ(2);
     else if (op <= 256) HDZ(4);
     else HDZ(HEAD_MAXO / 64);
 #undef HDZ
+    sp.add(dbp + L.off[i], 1, nbz, 0, Ot, o, o, 0, hd.d_bias, hd.d_bias, o);
   }
+  sp.launch(s);
   // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
   // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
   // (tn_dev: the GEMMs resolve S from the device value, GemmArgs::snum)
@@ -1404,7 +1588,7 @@ static int heads_backward_impl(const ggnn_dims* d, const ggnn_output_head* heads
   // (hidden a multiple of 64: each product in one launch with the output /
   // operand split at H; otherwise one launch per half)
   const bool one = H % 64 == 0;
-  const long KC = std::max<long>(256, ((rows + 47) / 48 + 31) & ~31L);
+  const long KC = head_dw_kc(rows);
   for (int half = 0; half < (one ? 1 : 2); ++half) {
     // [dhT | dh0] = dZ W^T  (B(k=j, n=c) = W[c][j]; K = Ot: padding columns are zeros)
     GemmArgs q = gg_args();
@@ -1422,7 +1606,10 @@ static int heads_backward_impl(const ggnn_dims* d, const ggnn_output_head* heads
     w.E = P<const float>(ws, L.Sx) + (long)half * H * Ot;
     w.Z = (int)((rows + KC - 1) / KC); w.M = one ? 2 * H : H; w.N = Ot; w.K = (int)KC; w.Ktot = rows; w.sKp = KC;
     if (one) { w.Am2 = h0; w.Msplit = H; }
+    // the row chunks' partials in a slab, summed in chunk order (deterministic)
+    w.slab = P<float>(ws, L.slab); w.sSlab = (long)w.M * Ot;
     if (int e = gg_launch<PREC_SPLIT>(w, false, false, false, -1, s)) return e;
+    slab_reduce(w, 1, w.Z, nullptr, 0, 0, 0, s);
   }
   for (int i = 0; i < nheads; ++i)
     hipLaunchKernelGGL(k_head_dw_out, dim3(grid1d((long)K * heads[i].o)), dim3(256), 0, s, dW + L.off[i], Ot, K,

@@ -92,7 +92,27 @@ struct GemmArgs {
   // (mbC = C)
   const uint32_t* mbits;
   int mbw, mbC;
+  // GG_ATOMIC with a slab (deterministic split-K, round 5): z stores its
+  // partial product at slab[z * sSlab + m * N + n] instead of adding into D;
+  // k_slab_reduce then sums each output's z's in z order.  (The pair dW chunk
+  // that is its channel's only one, zmask 2, still stores straight into D.)
+  float* slab;
+  long sSlab;
+  // with csum: the column sums as deterministic partials instead of atomics,
+  // cpart[(z * cslots + m / 32) * N + n] = the sum over one 32-row slice's
+  // stored values (cslots = ceil(M / 32); a wave covering several slices puts
+  // its sum in the first and zeros in the others), summed in (z, slice) order
+  // afterwards (k_sum_rows)
+  float* cpart;
+  int cslots;
 };
+// column-sum partial of the wave whose rows start at row mw and cover nsl
+// 32-row slices (GemmArgs::cpart)
+DEV void csum_part(const GemmArgs& a, int z, int mw, int nsl, int n, float cs) {
+  const int s0 = mw >> 5;
+  for (int i = 0; i < nsl; ++i)
+    if (s0 + i < a.cslots) a.cpart[((long)z * a.cslots + s0 + i) * a.N + n] = i ? 0.f : cs;
+}
 
 // exact power of two S <= t carrying the heads' dZ ~ 1/t into the f16 normal
 // range (frexp exponent e: S = 2^(e-1), clamped to 2^+-100); host and device
@@ -364,16 +384,60 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs a) {
             if (a.E) x *= a.E[doff];
             cs += x;
             float* d = (hi_n ? a.D2 : a.D) + doff;
-            if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-            else if (a.mode == GG_ADD) *d += x;
+            if (a.mode == GG_ATOMIC) {
+              if (a.slab) a.slab[(long)z * a.sSlab + (long)m * a.N + n] = x;
+              else atomicAdd(d, x);
+            } else if (a.mode == GG_ADD) *d += x;
             else *d = x;
           }
       }
       if (a.csum) {
         cs += __shfl_xor(cs, 32);
-        if (hh == 0 && n < a.N) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+        if (hh == 0 && n < a.N) {
+          if (a.cpart) csum_part(a, z, m0 + wm * 32 * WM, WM, n, cs);
+          else atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+        }
       }
     }
     __syncthreads();  // the next z's prologue rewrites buffer 0
   }
+}
+
+// ---- deterministic split-K reduction of slab partials (GemmArgs::slab):
+// group g's output (m, n) at D + g * sDg + m * sDm + n = (add ? D : 0) + the sum
+// of the partials of g's z's in (t, z) order, t < nt (slab z of t at
+// t * zT + z; nt = 1 for a product's own slab): z in [zs[g] / zsdiv,
+// zs[g+1] / zsdiv) (zs set) or [g * zper, (g + 1) * zper); z skipped where
+// zmask[z] == 0; sole: a group of one z stored its outputs itself (pair dW,
+// zmask 2) and is left alone; a group with no z writes nothing when adding,
+// zeros otherwise.
+struct SlabRed {
+  const float* slab;
+  long sSlab, zT;
+  float* D;
+  long sDg, sDm;
+  int M, N, G, zper, zsdiv, nt;
+  const int* zs;
+  const unsigned char* zmask;
+  int sole, add;
+};
+__global__ void __launch_bounds__(256) k_slab_reduce(SlabRed r) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= (long)r.M * r.N) return;
+  const int z0 = r.zs ? r.zs[g] / r.zsdiv : g * r.zper, z1 = r.zs ? r.zs[g + 1] / r.zsdiv : (g + 1) * r.zper;
+  if (r.sole && z1 - z0 == 1) return;
+  float s = 0.f;
+  bool any = false;
+  for (int t = 0; t < r.nt; ++t)
+    for (int z = z0; z < z1; ++z) {
+      if (r.zmask && !r.zmask[z]) continue;
+      const float x = r.slab[((long)t * r.zT + z) * r.sSlab + e];
+      s = any ? s + x : x;
+      any = true;
+    }
+  if (!any && r.add) return;
+  const int m = (int)(e / r.N), n = (int)(e % r.N);
+  float* d = r.D + (long)g * r.sDg + (long)m * r.sDm + n;
+  *d = r.add ? *d + s : s;
 }

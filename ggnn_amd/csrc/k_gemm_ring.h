@@ -395,7 +395,10 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           if (a.E) x *= EPI_PRE ? pre[EPI_PRE ? i : 0][r] : a.E[doff];
           cs += x;
           float* d = Dn + doff;
-          if (a.mode == GG_ATOMIC && !sole) atomicAdd(d, x);
+          if (a.mode == GG_ATOMIC && !sole) {
+            if (a.slab) a.slab[(long)z * a.sSlab + (long)m * a.N + n] = x;
+            else atomicAdd(d, x);
+          }
           else if (a.mode == GG_ADD) *d = (EPI_PRE ? pre[EPI_PRE ? i : 0][r] : *d) + x;
           else *d = x;
         }
@@ -403,7 +406,10 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     // column sums (GemmArgs::csum): lanes l and l + 32 hold the same column
     if (a.csum) {
       cs += __shfl_xor(cs, 32);
-      if (hh == 0 && n < a.N) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+      if (hh == 0 && n < a.N) {
+        if (a.cpart) csum_part(a, z, m0 + wm * AM * 32, AM, n, cs);
+        else atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+      }
     }
   }
 }
@@ -605,13 +611,15 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
       if (a.E) x *= pre[4 * qq + r4];
       cs += x;
       float* d = Dn + doff;
-      if (a.mode == GG_ATOMIC) atomicAdd(d, x);
-      else if (a.mode == GG_ADD) *d = pre[4 * qq + r4] + x;
+      if (a.mode == GG_ATOMIC) {
+        if (a.slab) a.slab[(long)z * a.sSlab + (long)m * a.N + n] = x;
+        else atomicAdd(d, x);
+      } else if (a.mode == GG_ADD) *d = pre[4 * qq + r4] + x;
       else *d = x;
     }
   }
   if (a.csum) {
     cs += __shfl_xor(cs, 32);
-    if (hh == 0) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+    if (hh == 0) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);  // (k_gemm_ks: no cpart callers)
   }
 }

@@ -178,11 +178,11 @@ __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict
 __global__ void __launch_bounds__(256) k_gen_bwd1(const float* __restrict__ d, const float* __restrict__ G,
                                                   const float* __restrict__ h, const float* __restrict__ cc,
                                                   float* __restrict__ dzc, float* __restrict__ dzg,
-                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ dbc,
-                                                  float* __restrict__ dbg) {
+                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ bpart) {
   // grid (column blocks, row slices): column k per thread, the slice's rows in
-  // turn; the bias gradients dbc = sum dzc, dbg[H:] = sum dzg_u as one atomic
-  // per column per block (no separate column-sum pass over dzc / dzg)
+  // turn; the bias gradients' slice partials sum dzg_u, sum dzc go to the
+  // slice's row of bpart ([slices][dbg_r | dbg_u | dbc], summed in a fixed
+  // order after the backward: k_sum_rows)
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= H) return;
   const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
@@ -198,15 +198,13 @@ __global__ void __launch_bounds__(256) k_gen_bwd1(const float* __restrict__ d, c
     sc += zc;
     su += zu;
   }
-  if (r1 > r0) {
-    atomicAdd(dbc + k, sc);
-    atomicAdd(dbg + H + k, su);
-  }
+  bpart[(long)blockIdx.y * 3 * H + H + k] = su;
+  bpart[(long)blockIdx.y * 3 * H + 2 * H + k] = sc;
 }
 // e2: d(rh) -> dr = d(rh) h, dzg_r = dr r(1-r); dh += d(rh) r; dbg[:H] += sum dzg_r
 __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh, const float* __restrict__ G,
                                                   const float* __restrict__ h, float* __restrict__ dzg,
-                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ dbg) {
+                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ bpart) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= H) return;
   const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
@@ -220,7 +218,7 @@ __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh,
     DXH[row * 2 * H + H + k] += x * r;
     sr += zr;
   }
-  if (r1 > r0) atomicAdd(dbg + k, sr);
+  bpart[(long)blockIdx.y * 3 * H + k] = sr;
 }
 // dL/dh_t (second half of DXH) -> the next (earlier) step's delta: the state
 // dropout backward of timestep tm = t-1 (tm < 0: none), times osc (the

@@ -256,7 +256,10 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
           float* __restrict__ dh_out, u16* __restrict__ dzcT, u16* __restrict__ dzgT,
-          float* __restrict__ dbc, float* __restrict__ dbg, long N, const uint32_t* __restrict__ gmax) {
+          float* __restrict__ dbc, float* __restrict__ dbg, long N, const uint32_t* __restrict__ gmax,
+          float* __restrict__ bpart) {
+  // bpart: this timestep's [workgroup][dbg (2H) | dbc (H)] rows of bias partials
+  // (summed in a fixed order by k_sum_rows: deterministic), or nullptr: atomics
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16, WH = SPLIT && GGNN_GB_WHI;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
   const float ds = gscale(gmax);  // gradient scale of dL/dh_T read in place (ggnn_common.h), else 1
@@ -310,7 +313,15 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   }
   csum += __shfl_xor(csum, 32);
   usum += __shfl_xor(usum, 32);
-  if (hh == 0) { atomicAdd(dbc + n, csum); atomicAdd(dbg + H + n, usum); }
+  if (hh == 0) {
+    if (bpart) {
+      bpart[(long)blockIdx.x * 3 * H + H + n] = usum;
+      bpart[(long)blockIdx.x * 3 * H + 2 * H + n] = csum;
+    } else {
+      atomicAdd(dbc + n, csum);
+      atomicAdd(dbg + H + n, usum);
+    }
+  }
   __syncthreads();
   TSMARK(1, 1);
 
@@ -361,7 +372,10 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     }
   }
   rsum += __shfl_xor(rsum, 32);
-  if (hh == 0) atomicAdd(dbg + n, rsum);
+  if (hh == 0) {
+    if (bpart) bpart[(long)blockIdx.x * 3 * H + n] = rsum;
+    else atomicAdd(dbg + n, rsum);
+  }
   __syncthreads();
   TSMARK(1, 3);
 

@@ -122,6 +122,121 @@ __global__ void __launch_bounds__(256) k_embed_bwd(EmbArgs a, EmbGrad gd, const 
   }
 }
 
+// ---- the deterministic form (ggnn_embed_backward_ws, round 5).  The lookups
+// add into a 64-bit fixed-point copy of each table (EMB_FX fractional bits):
+// integer addition does not depend on the order the atomics land in, so the
+// table gradient is the same bits run to run (and for any split of the
+// lookups).  Each looked-up row also records its owner, the first lookup row
+// of that id (atomicMax of rows - r); k_embed_fin then has the owner's wave
+// convert the row to fp32, clear it and release the owner slot, so the
+// workspace is all zeros again after every call (the caller zero-fills it
+// once).  Per-lookup squared norms: one partial per (block, segment), summed
+// in a fixed order by k_embed_fin's last block.  Range: |table gradient
+// element| < 2^23; resolution 2^-40.
+#define EMB_FX 40
+#define EMB_SQ_BLOCKS 4096  // k_embed_bwd_det blocks at most (one squared-norm partial row each)
+struct EmbAcc {
+  long long* acc[EMB_MAXSEG];  // [rows][width] fixed-point accumulator of segment s's table (shared per table)
+  int* own[EMB_MAXSEG];        // [rows] owner slots (emb_owner of the first lookup), 0 = none
+};
+// owner code of lookup (row r, segment s): the largest code is the smallest
+// row, then the smallest segment (segments sharing a table share the slots)
+DEV int emb_owner(long rows, long r, int s) { return (int)(((rows - r) << 3) | (EMB_MAXSEG - 1 - s)); }
+__global__ void __launch_bounds__(256) k_embed_bwd_det(EmbArgs a, EmbAcc ea, const int* __restrict__ wi,
+                                                       const float* __restrict__ dh0,
+                                                       const float* __restrict__ dh0_add, float* __restrict__ sqp) {
+  const Drop dr = drop_resolve(a.dr);
+  float acc[EMB_MAXSEG];
+#pragma unroll
+  for (int i = 0; i < EMB_MAXSEG; ++i) acc[i] = 0.f;
+  const long nq = (a.rows + 3) >> 2, total = nq * a.H;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long q = e / a.H;
+    const int k = (int)(e % a.H);
+    const int s = emb_find(a, k);
+    if (s < 0) continue;
+    const EmbSeg& S = a.s[s];
+    const uint4 w = dr.thr ? emb_words(dr, q * 4, k) : make_uint4(0u, 0u, 0u, 0u);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long r = q * 4 + i;
+      if (r >= a.rows) break;
+      float g = dh0[r * a.H + k] + (dh0_add ? dh0_add[r * a.H + k] : 0.f);
+      if (dr.thr) g = drop_apply(dr, u4_get(w, i), g);
+      const int id = wi[r * a.ncols + S.column];
+      if (id < 0 || id >= S.rows) continue;
+      const long long fx = __double2ll_rn((double)g * (double)(1LL << EMB_FX));
+      atomicAdd((unsigned long long*)(ea.acc[s] + (long)id * S.width + (k - S.offset)), (unsigned long long)fx);
+      if (k == S.offset) atomicMax(ea.own[s] + id, emb_owner(a.rows, r, s));
+      ss += g * g;
+    }
+#pragma unroll
+    for (int i = 0; i < EMB_MAXSEG; ++i)
+      if (i == s) acc[i] += ss;
+  }
+  __shared__ float red[4][EMB_MAXSEG];
+#pragma unroll
+  for (int i = 0; i < EMB_MAXSEG; ++i) {
+    float x = acc[i];
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][i] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < EMB_MAXSEG)
+    sqp[(long)blockIdx.x * EMB_MAXSEG + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+// one wave per (lookup row, segment): the owner converts its id's row into
+// d_table (zeroed before), clears the accumulator row and releases the slot;
+// the last block sums the squared-norm partials (nblk rows) per slot:
+// 256 threads over contiguous block ranges, then a fixed-order LDS tree
+__global__ void __launch_bounds__(256) k_embed_fin(EmbArgs a, EmbAcc ea, EmbGrad gd, const int* __restrict__ wi,
+                                                   const float* __restrict__ sqp, int nblk, float* __restrict__ sq) {
+  if (blockIdx.x == gridDim.x - 1) {
+    __shared__ float t[256][EMB_MAXSEG + 1];
+    const int per = (nblk + 255) / 256, b0 = threadIdx.x * per, b1 = min(nblk, b0 + per);
+    float v[EMB_MAXSEG];
+#pragma unroll
+    for (int i = 0; i < EMB_MAXSEG; ++i) v[i] = 0.f;
+    for (int b = b0; b < b1; ++b)
+#pragma unroll
+      for (int i = 0; i < EMB_MAXSEG; ++i) v[i] += sqp[(long)b * EMB_MAXSEG + i];
+#pragma unroll
+    for (int i = 0; i < EMB_MAXSEG; ++i) t[threadIdx.x][i] = v[i];
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+      if (threadIdx.x < h)
+#pragma unroll
+        for (int i = 0; i < EMB_MAXSEG; ++i) t[threadIdx.x][i] += t[threadIdx.x + h][i];
+      __syncthreads();
+    }
+    if (threadIdx.x < a.nseg) {
+      const int slot = threadIdx.x;
+      float x = 0.f;
+      for (int i = 0; i < a.nseg; ++i)
+        if (gd.sqslot[i] == slot) x += t[0][i];
+      sq[slot] = x;
+    }
+    return;
+  }
+  const long wv = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wv >= a.rows * a.nseg) return;
+  const long r = wv / a.nseg;
+  const int s = (int)(wv % a.nseg);
+  const EmbSeg& S = a.s[s];
+  const int id = wi[r * a.ncols + S.column];
+  if (id < 0 || id >= S.rows || ea.own[s][id] != emb_owner(a.rows, r, s)) return;
+  long long* ar = ea.acc[s] + (long)id * S.width;
+  float* dt = gd.dtable[s] + (long)id * S.width;
+  for (int k = lane; k < S.width; k += 64) {
+    dt[k] = (float)((double)ar[k] * (1.0 / (double)(1LL << EMB_FX)));
+    ar[k] = 0;
+  }
+  if (lane == 0) ea.own[s][id] = 0;
+}
+
 // ---------------------------------------------------------------------------
 // output heads
 // ---------------------------------------------------------------------------
@@ -231,16 +346,17 @@ __global__ void __launch_bounds__(256) k_head_softmax(const float* __restrict__ 
 }
 
 // dZ = g * (p * sum(y) - y) / num per row (d/dz of -sum y log softmax(z)), and
-// the bias gradient db[j] += sum_r dZ[r][j]: column partials in registers
-// (lane l owns columns l + 64i, o <= HEAD_MAXO), summed over the block's waves
-// in LDS, one global atomic per column per block
+// the bias gradient's block partials dbp[block * ldp + j] = sum over the
+// block's rows of dZ[r][j]: column partials in registers (lane l owns columns
+// l + 64i, o <= HEAD_MAXO), summed over the block's waves in LDS in wave order
+// (the blocks' rows are summed in block order afterwards: k_sum_rows)
 // (dZ: the head's columns of the concatenated [rows][ldz] array, padded to op
 // with zeros; the row's p and y held in registers)
 template <int NI>
 __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, const float* __restrict__ y, long rows,
                                                  int o, int op, float inv_num, const float* __restrict__ num_dev,
                                                  const float* __restrict__ dloss, float* __restrict__ dZ, int ldz,
-                                                 float* __restrict__ db) {
+                                                 float* __restrict__ dbp, int ldp) {
   __shared__ float cs[4][NI * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (num_dev) inv_num = 1.0f / *num_dev;
@@ -288,5 +404,5 @@ __global__ void __launch_bounds__(256) k_head_dz(const float* __restrict__ p, co
   for (int i = 0; i < NI; ++i)
     if (lane + 64 * i < o) cs[w][lane + 64 * i] = part[i];
   __syncthreads();
-  for (int j = threadIdx.x; j < o; j += 256) atomicAdd(db + j, cs[0][j] + cs[1][j] + cs[2][j] + cs[3][j]);
+  for (int j = threadIdx.x; j < o; j += 256) dbp[(long)blockIdx.x * ldp + j] = ((cs[0][j] + cs[1][j]) + cs[2][j]) + cs[3][j];
 }

@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(1024) k_pair_scan(const u16* __restrict__ degc
 __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pcnt, int C, int cap_tiles, int zw_cap,
                                                       int* __restrict__ poff, int* __restrict__ ptile,
                                                       unsigned char* __restrict__ pmask, int* __restrict__ wtl,
-                                                      int* __restrict__ wmap, unsigned char* __restrict__ wmask) {
+                                                      int* __restrict__ wmap, unsigned char* __restrict__ wmask,
+                                                      int* __restrict__ wst) {
   __shared__ int soff[CHL_MAXC + 1], cst[CHL_MAXC + 1];
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -108,7 +109,10 @@ __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pc
     cst[C] = ch;
   }
   __syncthreads();
-  for (int c = tid; c <= C; c += blockDim.x) poff[c] = soff[c];
+  for (int c = tid; c <= C; c += blockDim.x) {
+    poff[c] = soff[c];
+    wst[c] = cst[c];  // channel c's dW chunks: [wst[c], wst[c+1]) (k_slab_reduce)
+  }
   const int live_tiles = soff[C] / PAIR_TILE;
   // the channel of a tile / chunk: the last c with start <= x (binary search)
   auto find = [&](const int* st, int x) {
@@ -380,20 +384,20 @@ __global__ void k_pair_gather_dx(const int* __restrict__ prow, const unsigned ch
   }
 }
 
-// dbeta[c][k] += sum over c's pair rows of deg_p dXg[p][k]: grid (column
-// blocks, C, row slices), one atomic per column per block
-__global__ void __launch_bounds__(256) k_pair_dbeta(const int* __restrict__ poff, const int* __restrict__ pcnt,
+// dL/dbeta partials: part[tile][k] = sum over the pair tile's rows (one
+// channel's, padding rows of degree 0) of deg_p dXg[p][k]; grid (column
+// blocks, pair tiles).  The channels' sums over their tiles (and the
+// timesteps) follow in a fixed order (k_slab_reduce): no atomics.
+__global__ void __launch_bounds__(256) k_pair_dbeta(const unsigned char* __restrict__ pmask,
                                                     const float* __restrict__ pdeg, const float* __restrict__ dXg,
-                                                    float* __restrict__ dbeta, int H) {
-  const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
-  if (k >= H) return;
-  const int n = pcnt[c], p0 = poff[c];
-  const int per = max(16, (n + gridDim.z - 1) / gridDim.z), a = blockIdx.z * per, e = min(n, a + per);
-  if (a >= e) return;
+                                                    float* __restrict__ part, int H) {
+  const int k = blockIdx.x * 256 + threadIdx.x, tile = blockIdx.y;
+  if (k >= H || !pmask[tile]) return;
+  const long p0 = (long)tile * PAIR_TILE;
   float s = 0.f;
 #pragma unroll 4
-  for (int p = p0 + a; p < p0 + e; ++p) s += pdeg[p] * dXg[(long)p * H + k];
-  atomicAdd(dbeta + (long)c * H + k, s);
+  for (int i = 0; i < PAIR_TILE; ++i) s += pdeg[p0 + i] * dXg[(p0 + i) * H + k];
+  part[(long)tile * H + k] = s;
 }
 
 // B3: DXH[g*v+j][H + k] += sum over the channels c of g (ascending) and the

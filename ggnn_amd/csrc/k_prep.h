@@ -265,16 +265,67 @@ __global__ void k_dropout_mask(int kind, int C, int H, int b, int vin, int t, Dr
   }
 }
 
-// out[e] += sum_g part[g][e]  (dL/dbeta from k_prop_bwd's per-(timestep, graph)
-// partials): blockIdx.y takes a slice of the rows, one atomic per slice
-__global__ void k_sum_graphs(const float* __restrict__ part, float* __restrict__ out, int rows, long E) {
-  const int per = (rows + gridDim.y - 1) / gridDim.y;
-  const int g0 = blockIdx.y * per, g1 = min(rows, g0 + per);
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int g = g0; g < g1; ++g) s += part[(long)g * E + e];
-    if (g1 > g0) atomicAdd(out + e, s);
+// Column sums of row partials in a fixed order (deterministic: no atomics).
+// Element e in [0, E) = (ec, ek) = (e / Nc, e % Nc); row (t, w), t < T, w < nw,
+// holds it at part[t * sT + w * sW + ec * sC + ek]; a row is skipped where
+// mask && !mask[t * mT + ec * mC].  out = (add ? out : 0) + the sum over the
+// rows in (t, w) order, columns e < split to out0[e], the others to
+// out1[e - split].  Uses: dL/dbeta from k_prop_bwd's per-(timestep, graph)
+// partials, dL/dbg and dL/dbc from k_gru_bwd's per-(timestep, workgroup) rows,
+// the general path's bias partials, the heads' bias columns.  Two launches:
+// k_sum_rows sums row chunk rc of 64 columns per block (4 waves on
+// interleaved rows, combined in wave order) into scratch[rc][E];
+// k_sum_rows_fin adds the chunks in chunk order.
+#define SUMJ_MAX 4
+struct SumJob {
+  const float* part;
+  float* out0;
+  float* out1;
+  float* scratch;  // [rcs][E]
+  const unsigned char* mask;
+  long sT, sW, sC, mT, mC, E, Nc, split;
+  int T, nw, rcs, add;  // rcs: row chunks
+};
+struct SumJobs {
+  SumJob j[SUMJ_MAX];
+  int bx[SUMJ_MAX + 1];  // first block of each job (k_sum_rows: colgroups * rcs blocks)
+  int fx[SUMJ_MAX + 1];  // first block of each job (k_sum_rows_fin: E / 256 blocks)
+  int count;
+};
+__global__ void __launch_bounds__(256) k_sum_rows(SumJobs js) {
+  int ji = 0;
+  while (ji + 1 < js.count && js.bx[ji + 1] <= (int)blockIdx.x) ++ji;
+  const SumJob& J = js.j[ji];
+  const int lb = blockIdx.x - js.bx[ji], cg = lb / J.rcs, rc = lb % J.rcs;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long e = (long)cg * 64 + lane;
+  const long rows = (long)J.T * J.nw, per = (rows + J.rcs - 1) / J.rcs;
+  const long r0 = rc * per, r1 = min(rows, r0 + per);
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (e < J.E) {
+    const long ec = e / J.Nc, eo = ec * J.sC + e % J.Nc;
+#pragma unroll 4
+    for (long r = r0 + w; r < r1; r += 4) {
+      const long t = r / J.nw, ww = r % J.nw;
+      if (J.mask && !J.mask[t * J.mT + ec * J.mC]) continue;
+      s += J.part[t * J.sT + ww * J.sW + eo];
+    }
   }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && e < J.E) J.scratch[(long)rc * J.E + e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+__global__ void __launch_bounds__(256) k_sum_rows_fin(SumJobs js) {
+  int ji = 0;
+  while (ji + 1 < js.count && js.fx[ji + 1] <= (int)blockIdx.x) ++ji;
+  const SumJob& J = js.j[ji];
+  const long e = (long)(blockIdx.x - js.fx[ji]) * 256 + threadIdx.x;
+  if (e >= J.E) return;
+  float s = J.scratch[e];
+  for (int rc = 1; rc < J.rcs; ++rc) s += J.scratch[(long)rc * J.E + e];
+  float* o = e < J.split ? J.out0 + e : J.out1 + (e - J.split);
+  *o = J.add ? *o + s : s;
 }
 
 // Training-forward staging of h0 in one pass: h0 [b][vin][H] fp32 -> hf [N][H]

@@ -6,8 +6,13 @@
 // chem_tensorflow.py:496):
 //   d gates_kernel     = [X | h]^T  dzg        d candidate_kernel = [X | r*h]^T dzc
 //   d edge_weights[c]  = h^T dM_c
-// Each workgroup sums its K chunk over all T steps, then issues one fp32
-// atomicAdd per output element (chip-wide atomic bytes: tiles * chunks * 64 KiB).
+// Each workgroup sums its K chunk over all T steps.  Deterministic reduction
+// over the K chunks (WgArgs::part, round 5): the workgroup stores its partial
+// tile in the accumulator's own register order (16-byte stores, one
+// [TS][TS] block per (tile, chunk)), and k_wgrad_reduce sums the chunks of a
+// tile in chunk order and writes the output once -- the same bits whatever
+// order the workgroups ran in (with part == nullptr: one fp32 atomicAdd per
+// output element and chunk, order-dependent).
 #pragma once
 #include "ggnn_common.h"
 
@@ -33,7 +38,65 @@ struct WgArgs {
   WgProb p[WG_MAXP];
   int nprob, nchunks, KC;
   int H;  // rows of one operand array (wg_off layout); ldP / ldQ hold its N
+  float* part;  // [tiles][nchunks][TS * TS] partial tiles (deterministic reduction), or nullptr: atomics
 };
+
+// (problem, batch index, tile origin) of tile `tile` (TS x TS tiles)
+struct WgTile {
+  int pi, bi, m0, n0;
+};
+template <int TS>
+DEV WgTile wg_tile(const WgArgs& args, int tile) {
+  int pi = 0;
+  while (pi + 1 < args.nprob && args.p[pi + 1].tile_begin <= tile) ++pi;
+  const WgProb& pr = args.p[pi];
+  const int lt0 = tile - pr.tile_begin;
+  const int lt = lt0 % pr.tiles_b;
+  return WgTile{pi, lt0 / pr.tiles_b, (lt / pr.tiles_n) * TS, (lt % pr.tiles_n) * TS};
+}
+
+// A workgroup's partial tile in accumulator order: float4 index
+// f = ((((wave * NI + i) * NJ + j) * 4 + quad) * 64 + lane) holds rows
+// acc_row(4 quad + e, lane >> 5) of the (wave, i, j) 32 x 32 block, column lane & 31
+template <int NI, int NJ>
+DEV void wg_store_part(float* pp, const f32x16 (&acc)[NI][NJ], int wv, int lane) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *(float4*)(pp + ((((wv * NI + i) * NJ + j) * 4 + q) * 64 + lane) * 4) =
+            make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+}
+
+// out = sum over the K chunks of the partial tiles, in chunk order.  TS = 256:
+// k_wgrad256's 8 waves as 2 (m) x 4 (n) of 128 x 64 (NI = 4, NJ = 2); TS = 128:
+// k_wgrad's 4 waves as 2 x 2 of 64 x 64 (NI = NJ = 2).  One thread per float4
+// of a tile; grid = tiles * TS * TS / 1024 blocks of 256.
+template <int TS>
+__global__ void __launch_bounds__(256) k_wgrad_reduce(WgArgs args) {
+  constexpr int NI = TS == 256 ? 4 : 2, NJ = 2, WN = TS == 256 ? 4 : 2, WMR = NI * 32, WNC = NJ * 32;
+  constexpr int BPT = TS * TS / 1024;  // blocks per tile
+  const int tile = blockIdx.x / BPT;
+  const int f = (blockIdx.x % BPT) * 256 + threadIdx.x;
+  const float* src = args.part + (long)tile * args.nchunks * (TS * TS) + f * 4;
+  float4 s = *(const float4*)src;
+  for (int c = 1; c < args.nchunks; ++c) {
+    const float4 x = *(const float4*)(src + (long)c * (TS * TS));
+    s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+  }
+  const WgTile wt = wg_tile<TS>(args, tile);
+  const WgProb& pr = args.p[wt.pi];
+  const int lane = f & 63, q = (f >> 6) & 3, j = (f >> 8) % NJ, i = (f >> 8) / NJ % NI, wv = (f >> 8) / (NJ * NI);
+  const int m = wt.m0 + (wv / WN) * WMR + i * 32 + acc_row(4 * q, lane >> 5);
+  const int nn = wt.n0 + (wv % WN) * WNC + j * 32 + (lane & 31);
+  float* o = pr.out + (long)wt.bi * pr.sOb + (long)m * pr.ldO + nn;
+  o[0] = s.x;
+  o[pr.ldO] = s.y;
+  o[2L * pr.ldO] = s.z;
+  o[3L * pr.ldO] = s.w;
+}
 
 template <int BK, int PREC>
 __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
@@ -144,6 +207,10 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
     if (pre) sstore((it + 1) & 1);
     __syncthreads();
   }
+  if (args.part) {
+    wg_store_part<2, 2>(args.part + (long)blockIdx.x * (128 * 128), acc, wv, lane);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -221,7 +288,7 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
     }
   }
   const int nit = kits * pr.T;
-  if (nit == 0) return;
+  if (nit == 0 && !args.part) return;  // (partials: a zero tile still has to be stored)
   // row of slice `it`'s first K element: graph glr[i] (i = slice / V32) row (slice % V32) * 32
   auto krow = [&](int sl) -> long {
     if (!listed) return kbase + (long)sl * BK;
@@ -287,6 +354,10 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
     for (int u = 0; u < NBUF; ++u) slice(it0 + u, u);
   }
   for (int u = 0; u < nit - nfull; ++u) slice(nfull + u, u);
+  if (args.part) {
+    wg_store_part<4, 2>(args.part + (long)blockIdx.x * (256 * 256), acc, wv, lane);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -74,9 +74,27 @@ class EmbeddingFrontEnd:
     concat order.  btb: [(loc_embeddings, 0), (pos_embeddings, 1),
     (word_embeddings, 2), (loc_embeddings, 3)] (:268-299)."""
 
-    def __init__(self, hidden: int):
+    def __init__(self, hidden: int, deterministic: bool = True):
+        """deterministic: the table gradients through ggnn_embed_backward_ws
+        (fixed-point accumulation: the same bits run to run); False: the fp32
+        atomics of ggnn_embed_backward."""
         self.hidden = int(hidden)
         self._lib = _lib.load()
+        self.deterministic = bool(deterministic) and hasattr(self._lib, "ggnn_embed_backward_ws")
+        self._ws = {}    # table set -> zero-filled workspace (each call leaves it zero-filled)
+
+    def workspace(self, segments, device):
+        """The deterministic backward's workspace for this table set: allocated
+        (zero-filled) once and kept, so a captured step's pointer stays valid."""
+        key = tuple((t.data_ptr(), tuple(t.shape)) for t, _ in segments)
+        ws = self._ws.get(key)
+        if ws is None:
+            n = ctypes.c_size_t(0)
+            _lib.check(self._lib.ggnn_embed_workspace_bytes(self._segs(segments), len(segments), ctypes.byref(n)),
+                       "ggnn_embed_workspace_bytes")
+            ws = torch.zeros(max(int(n.value), 1), dtype=torch.uint8, device=device)
+            self._ws[key] = ws
+        return ws
 
     def _segs(self, segments, dtables=None):
         arr = (EmbedSegment * len(segments))()
@@ -108,12 +126,14 @@ class EmbeddingFrontEnd:
         dts = dtables if dtables is not None else [torch.empty_like(t) for t, _ in segments]
         sq = sq_out if sq_out is not None else torch.empty(len(segments), dtype=torch.float32, device=wi.device)
         d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32", seed_device=seed_device)
-        _lib.check(self._lib.ggnn_embed_backward(ctypes.byref(d), self._segs(segments, dts), len(segments), _ptr(wi),
-                                                 ncols, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                                                 _ptr(dh0.contiguous()), _ptr(None if dh0_add is None else
-                                                                              dh0_add.contiguous()),
-                                                 _ptr(sq), _stream()),
-                   "ggnn_embed_backward")
+        args = (ctypes.byref(d), self._segs(segments, dts), len(segments), _ptr(wi), ncols, float(keep),
+                int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dh0.contiguous()),
+                _ptr(None if dh0_add is None else dh0_add.contiguous()), _ptr(sq))
+        if self.deterministic:
+            _lib.check(self._lib.ggnn_embed_backward_ws(*args, _ptr(self.workspace(segments, wi.device)), _stream()),
+                       "ggnn_embed_backward_ws")
+        else:
+            _lib.check(self._lib.ggnn_embed_backward(*args, _stream()), "ggnn_embed_backward")
         return dts, sq
 
 

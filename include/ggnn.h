@@ -298,6 +298,21 @@ int ggnn_embed_backward(const ggnn_dims* d, const ggnn_embed_segment* segs, int 
                         const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
                         const float* dh0, const float* dh0_add, float* lookup_sqnorm,
                         ggnn_stream_t stream);
+/* The same, bit-reproducible (round 5): the lookups accumulate into a 64-bit
+ * fixed-point copy of each table (2^-40 resolution, |element| < 2^23), whose
+ * integer sums do not depend on the order the additions land in, and the
+ * squared norms are summed in a fixed order.  ws: a device buffer of
+ * ggnn_embed_workspace_bytes (which depends on the tables only, not on the
+ * batch), ZERO-FILLED by the caller before its first use; every call leaves it
+ * zero-filled again.  Segments sharing a d_table (which must then have one
+ * shape) accumulate together, as in ggnn_embed_backward.  (ggnn_embed_backward
+ * above adds fp32 atomics: its result can differ in the last bits from run to
+ * run.) */
+int ggnn_embed_workspace_bytes(const ggnn_embed_segment* segs, int nseg, size_t* bytes);
+int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg,
+                           const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
+                           const float* dh0, const float* dh0_add, float* lookup_sqnorm, void* ws,
+                           ggnn_stream_t stream);
 
 /* Output heads: gated_regression for --pr btb, chem_tensorflow_dense.py:439-516
  * with MLP(2h, o, [], out_layer_dropout_keep_prob) (utils.py:40-84), and the

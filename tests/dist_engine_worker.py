@@ -35,7 +35,7 @@ def main():
     w = O.synthetic_weights(h, C, seed=21)
     rng = np.random.default_rng(22)
     dhT = [(rng.standard_normal((b, v, h)) * 2.0 ** -8).astype(np.float32) for _ in range(2)]
-    eps = 1e-3  # see tests/test_gpu_dist.py
+    eps = 1e-8  # the reference's Adam epsilon (chem_tensorflow.py:494)
 
     def dev_t(x):
         return torch.from_numpy(np.ascontiguousarray(x)).to(dev)

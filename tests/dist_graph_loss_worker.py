@@ -22,7 +22,6 @@ def main():
     import torch.distributed as tdist
     from ggnn_amd.dist import all_reduce_sum, init_from_env
     from ggnn_amd.model import DenseGGNNChemModel
-    from ggnn_amd.optim import ClipAdam
 
     rank, world, _ = init_from_env("gloo")
     torch.cuda.set_device(0)
@@ -39,7 +38,7 @@ def main():
                                bucket_max_nodes=int(g["bucket_max_nodes"]), precision="fp32", vocab_size=vocab,
                                embedding_sizes=dict(loc=16, pos=8, word=16, edge=8), seed=5, rank=rank,
                                world_size=world)
-        m.optimizer = ClipAdam(m.trainable_variables(), learning_rate=0.003, epsilon=1e-3)
+        # (Adam as the reference configures it: epsilon 1e-8, chem_tensorflow.py:494)
         return m
 
     mg, me = model(True), model(False)

@@ -50,15 +50,15 @@ def test_two_rank_engine_step_equals_full_batch(tmp_path, shape):
         ref = d["full_grads"][s]
         err = np.abs(d["dp_grads"][s] - ref).max() / np.abs(ref).max()
         assert err <= 1e-4, (s, err)
-    # and so do the weights after two clip + Adam steps.  Adam's epsilon is
-    # raised to 1e-3 here (reference: 1e-8): with 1e-8, g / sqrt(v) turns
-    # reduction-order differences of ~1e-7 in near-zero gradient elements into
-    # +-lr flips, which says nothing about the data-parallel path
-    # (ClipAdam itself is pinned against the oracle in test_gpu_parity.py).
+    # and so do the weights after two clip + Adam steps at the reference's
+    # epsilon 1e-8 (chem_tensorflow.py:494)
     step_dp = d["dp_params"] - d["init"]
     step_full = d["full_params"] - d["init"]
     assert np.abs(step_full).max() > 1e-4   # the weights did move
-    assert np.abs(d["dp_params"] - d["full_params"]).max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
+    diff = np.abs(d["dp_params"] - d["full_params"])
+    print("engine dp vs full (Adam epsilon 1e-8): max param diff %.3g, elements > 1e-6: %d of %d"
+          % (diff.max(), int((diff > 1e-6).sum()), diff.size))
+    assert diff.max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
     assert np.abs(step_dp - step_full).max() <= 1e-3 * np.abs(step_full).max()
 
 
@@ -92,7 +92,10 @@ def test_two_rank_btb_train_step_equals_union_batch(tmp_path, hidden):
     np.testing.assert_allclose(d["dp_loss"], d["full_loss"], rtol=1e-5)
     step_full = d["full_params"] - d["init"]
     assert np.abs(step_full).max() > 1e-4
-    assert np.abs(d["dp_params"] - d["full_params"]).max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
+    diff = np.abs(d["dp_params"] - d["full_params"])
+    print("dp vs union (Adam epsilon 1e-8): max param diff %.3g, elements > 1e-6: %d of %d"
+          % (diff.max(), int((diff > 1e-6).sum()), diff.size))
+    assert diff.max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
     # run_epoch with world_size 2: every batch of the single-process schedule
     # ran once (steps summed over the ranks), finite loss, LAS/UAS fractions
     tr_loss, tr_ips, tr_steps, tr_las, tr_uas, va_loss, va_ips, va_steps, va_las, va_uas, n_tr, n_va = d["epoch"]
@@ -162,8 +165,10 @@ def test_two_rank_captured_step_returns_the_union_loss(tmp_path):
     _spawn("dist_graph_loss_worker.py", [out], tmp_path)
     d = np.load(out)
     assert int(d["uncaptured"]) == 1 and int(d["replayed"]) == 2 and int(d["eager_steps"]) == 3
-    np.testing.assert_allclose(d["graph_loss"], d["eager_loss"], rtol=1e-5)
-    assert float(d["param_diff"]) <= 1e-5 * max(float(d["param_scale"]), 1.0)
+    # the same launches in the same order, every reduction order-fixed: the
+    # same bits (Adam at the reference's epsilon 1e-8)
+    assert np.array_equal(d["graph_loss"], d["eager_loss"]), (d["graph_loss"], d["eager_loss"])
+    assert float(d["param_diff"]) == 0.0
 
 
 def test_rccl_one_rank_group_runs_the_training_collectives(tmp_path):
@@ -187,9 +192,10 @@ def test_rccl_one_rank_group_runs_the_training_collectives(tmp_path):
     for tag in ("eager", "captured"):
         assert res[tag + "_train_buffer_unchanged"], tag
         la, l1 = res[tag + "_losses"]
-        np.testing.assert_allclose(la, l1, rtol=1e-6)
-        # (the two models' backward atomics sum in different orders)
-        assert res[tag + "_param_max_diff"] <= 1e-5 * max(res[tag + "_param_scale"], 1.0), (tag, res)
+        # a one-rank sum changes nothing and every reduction is order-fixed:
+        # the two models stay bit-identical through Adam at epsilon 1e-8
+        assert la == l1, (tag, la, l1)
+        assert res[tag + "_param_max_diff"] == 0.0, (tag, res)
     assert res["captured_graph_stats"]["replayed"] == 2
     assert res["destroyed"]
 

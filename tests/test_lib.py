@@ -75,5 +75,9 @@ def test_dropout_dims_validation_and_sizes(lib):
     # (T-1) extra masked copies of W and W^T (hi + lo limbs) and of the general path's fp32 W
     assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4)
     assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
-    assert _lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True) == 5 * 8 * 256 * 256 * 4
+    # + the per-timestep dW scratch G [T][C][h][h], and the (T-1) C extra
+    # per-timestep dW tiles' split-K partials (16 K chunks at b = 256, v = 128:
+    # k_wgrad_reduce's deterministic reduction)
+    assert (_lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True)
+            == 5 * 8 * 256 * 256 * 4 + 4 * 8 * 16 * 256 * 256 * 4)
     assert _lib.workspace_bytes(d2, False) == _lib.workspace_bytes(d1, False)
