@@ -29,7 +29,7 @@ EXPORTED = (
     "ggnn_set_adjacency_edges",
     "ggnn_forward", "ggnn_backward", "ggnn_adam_step", "ggnn_dropout_mask", "ggnn_kernel_kind_name", "ggnn_profile_begin",
     "ggnn_profile_end", "ggnn_embed_forward", "ggnn_embed_backward", "ggnn_embed_workspace_bytes",
-    "ggnn_embed_backward_ws", "ggnn_heads_workspace_bytes",
+    "ggnn_embed_backward_ws", "ggnn_embed_lookup_rows", "ggnn_heads_workspace_bytes",
     "ggnn_heads_forward", "ggnn_heads_backward", "ggnn_dbg_gemm", "ggnn_dbg_gemm_ex",
     "ggnn_adam_step_dev", "ggnn_heads_forward_dev", "ggnn_heads_backward_dev",
 )
@@ -112,6 +112,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
             lib.ggnn_embed_workspace_bytes.argtypes = [_P, _I, ctypes.POINTER(ctypes.c_size_t)]
             lib.ggnn_embed_backward_ws.restype = _I
             lib.ggnn_embed_backward_ws.argtypes = [_DP, _P, _I, _P, _I, F, U64, _P, _P, _P, _P, _P]
+            lib.ggnn_embed_lookup_rows.restype = _I
+            lib.ggnn_embed_lookup_rows.argtypes = [_DP, _P, _I, _I, _P, _I, F, U64, _P, _P, _P, _P,
+                                                   ctypes.c_int64, _P]
         lib.ggnn_heads_workspace_bytes.restype = _I
         lib.ggnn_heads_workspace_bytes.argtypes = [_DP, _P, _I, ctypes.POINTER(ctypes.c_size_t)]
         lib.ggnn_heads_forward.restype = _I

@@ -542,7 +542,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     z.add(P<float>(ws, L.gmax), 1);
   }
   const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
-  float* Dl = P<float>(ws, L.Dl);
   float* DXH = P<float>(ws, L.DXH);
   float* DRH = P<float>(ws, L.DRH);
   float* dM = P<float>(ws, L.M);
@@ -550,8 +549,6 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(N * H / 4 + 1), 1024)), dim3(256), 0, s, dhT, N * H,
                        P<uint32_t>(ws, L.gmax));
-    hipLaunchKernelGGL(k_gen_delta0, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, dhT, Dl, N, c.H, c.vin, c.sdrop, c.T - 1,
-                       gmax);
   }
   if (c.sparse) {
     Prof p(K_PROP_BWD, s);
@@ -573,8 +570,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     float* gbp = P<float>(ws, L.GBP) + (size_t)t * ewg.y * 3 * H;  // this timestep's bias partial rows
     {
       Prof p(K_GRU_BWD, s);
-      hipLaunchKernelGGL(k_gen_bwd1, ewg, dim3(256), 0, s, Dl, G, ht, P<const float>(ws, L.cc(t)), DZC, DZG, DXH, N,
-                         c.H, gbp);
+      // delta of step t: S * dL/dh_T at the last step, else the dh step t + 1
+      // left in DXH's second half; the state dropout of timestep t
+      const bool last_t = t == c.T - 1;
+      hipLaunchKernelGGL(k_gen_bwd1, ewg, dim3(256), 0, s, last_t ? dhT : DXH + H, last_t ? H : 2 * H,
+                         last_t ? gmax : (const uint32_t*)nullptr, c.sdrop, t, (int)c.vin, G, ht,
+                         P<const float>(ws, L.cc(t)), DZC, DZG, DXH, N, c.H, gbp);
     }
     // [dX1 | d(rh)] = dzc Wc^T  (Wc [2H][H]: B(k, n) = Wc[n][k]), one launch
     // over both halves: columns n >= H go to d(rh) (a separate [N][H] buffer)
@@ -609,16 +610,23 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       {
         Prof p(K_PROP_BWD, s);
         gen_pairs_y(c, AL, adj, ht, PY, s);
-        hipLaunchKernelGGL(k_pair_gather_dx, dim3(grid1d((long)AL.cap_tiles * PAIR_TILE * (H / 4))), dim3(256), 0, s,
-                           P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask), DXH, PDX,
-                           AL.cap_tiles * PAIR_TILE,
-                           c.H);
-        if (use_bias)
-          // per pair tile (one channel's rows): sum of deg * dXg, summed per
-          // channel in tile order after the timestep loop
-          hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)AL.cap_tiles), dim3(256), 0, s,
-                             P<const unsigned char>(adj, AL.pmask), P<const float>(adj, AL.pdeg), PDX,
-                             P<float>(ws, L.PDB) + (size_t)t * AL.cap_tiles * H, c.H);
+        // dXg gathered, with the dbeta partial of every pair tile (one
+        // channel's rows): sum of deg * dXg, summed per channel in tile order
+        // after the timestep loop
+        if (H <= 1024)
+          hipLaunchKernelGGL(k_pair_gather_dx_dbeta, dim3((unsigned)AL.cap_tiles), dim3(256), 0, s,
+                             P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask),
+                             P<const float>(adj, AL.pdeg), DXH, PDX,
+                             use_bias ? P<float>(ws, L.PDB) + (size_t)t * AL.cap_tiles * H : (float*)nullptr, c.H);
+        else {
+          hipLaunchKernelGGL(k_pair_gather_dx, dim3(grid1d((long)AL.cap_tiles * PAIR_TILE * (H / 4))), dim3(256), 0,
+                             s, P<const int>(adj, AL.prow), P<const unsigned char>(adj, AL.pmask), DXH, PDX,
+                             AL.cap_tiles * PAIR_TILE, c.H);
+          if (use_bias)
+            hipLaunchKernelGGL(k_pair_dbeta, dim3((unsigned)((H + 255) / 256), (unsigned)AL.cap_tiles), dim3(256), 0,
+                               s, P<const unsigned char>(adj, AL.pmask), P<const float>(adj, AL.pdeg), PDX,
+                               P<float>(ws, L.PDB) + (size_t)t * AL.cap_tiles * H, c.H);
+        }
       }
       if (int e = gen_pairs_product<PREC>(c, AL, adj, PDX, P<float>(pack, PL.gw(c.ed ? t : 0)), true, PZ, K_PROP_BWD,
                                           s))
@@ -684,11 +692,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
                            c.C, c.H, t, c.edrop);
     }
     }
-    // delta of step t-1 (state dropout of t-1), or dL/dh0 (unscaled)
-    {
+    // dL/dh0 (unscaled) after the first timestep; the earlier steps' deltas
+    // are formed inside the next k_gen_bwd1
+    if (t == 0) {
       Prof p(K_PROP_BWD, s);
-      hipLaunchKernelGGL(k_gen_delta, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, DXH, t == 0 ? dh0 : Dl, N, c.H, c.vin,
-                         c.sdrop, t - 1, gmax, t == 0 ? 1 : 0);
+      hipLaunchKernelGGL(k_gen_delta, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, DXH, dh0, N,
+                         c.H, c.vin, c.sdrop, -1, gmax, 1);
     }
   }
   if (c.sparse) {

@@ -1396,8 +1396,8 @@ int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, i
   memset(&gd, 0, sizeof(gd));
   memset(&ea, 0, sizeof(ea));
   for (int i = 0; i < nseg; ++i) {
-    if (!segs[i].d_table) return fail(GGNN_EINVAL, "embed_backward_ws: NULL d_table");
     gd.dtable[i] = segs[i].d_table;
+    if (!segs[i].d_table) continue;  // no gradient for this segment (its sq slot: 0)
     // segments sharing a d_table (btb: the loc table, word_inputs columns 0
     // and 3) accumulate in the first one's region; its squared norm slot too
     int u = i;
@@ -1415,7 +1415,8 @@ int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, i
   Prof p(K_HEADS, s);
   {
     Zeroer z(s);
-    for (int i = 0; i < nseg; ++i) z.add(segs[i].d_table, (long)segs[i].rows * segs[i].width);
+    for (int i = 0; i < nseg; ++i)
+      if (segs[i].d_table) z.add(segs[i].d_table, (long)segs[i].rows * segs[i].width);
   }
   const int nblk = std::min(grid1d((a.rows + 3) / 4 * a.H), EMB_SQ_BLOCKS);
   float* sqp = P<float>(ws, L.sqp);
@@ -1423,6 +1424,22 @@ int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, i
   const long waves = a.rows * nseg;
   hipLaunchKernelGGL(k_embed_fin, dim3((unsigned)((waves + 3) / 4 + 1)), dim3(256), 0, s, a, ea, gd, word_inputs, sqp,
                      nblk, lookup_sqnorm);
+  LAUNCHCHK();
+  return GGNN_OK;
+}
+
+int ggnn_embed_lookup_rows(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, int seg,
+                           const int32_t* word_inputs, int ncols, float keep, uint64_t seed, const float* dh0,
+                           const float* dh0_add, float* rows, int32_t* ids, int64_t cap, ggnn_stream_t stream) {
+  EmbArgs a;
+  if (int e = emb_args(d, segs, nseg, ncols, keep, seed, &a, "embed_lookup_rows")) return e;
+  if (seg < 0 || seg >= nseg) return fail(GGNN_EINVAL, "embed_lookup_rows: segment out of range");
+  if (!word_inputs || !dh0 || !rows || !ids) return fail(GGNN_EINVAL, "embed_lookup_rows: NULL pointer");
+  if (cap < a.rows) return fail(GGNN_EINVAL, "embed_lookup_rows: cap < b * v lookup rows");
+  hipStream_t s = (hipStream_t)stream;
+  Prof p(K_HEADS, s);
+  hipLaunchKernelGGL(k_embed_rows, dim3(grid1d(cap * segs[seg].width)), dim3(256), 0, s, a, seg, word_inputs, dh0,
+                     dh0_add, rows, ids, (long)cap);
   LAUNCHCHK();
   return GGNN_OK;
 }

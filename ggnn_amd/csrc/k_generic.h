@@ -175,22 +175,38 @@ __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict
 // ---- backward element-wise steps, timestep t (Appendix A of SURVEY.md):
 // e1: dc = d(1-u); du = d(h-c); dzc = dc(1-c^2); dzg_u = du u(1-u);
 //     dh (second half of the [N][2H] buffer DXH) = d u
-__global__ void __launch_bounds__(256) k_gen_bwd1(const float* __restrict__ d, const float* __restrict__ G,
+// with the step's delta d formed on the fly (round 5: no k_gen_delta /
+// k_gen_delta0 launch in front of it): d = din[row * ldin + k] * gscale(gmax)
+// through the state dropout of timestep tm (tm < 0: none) -- din = dL/dh_T
+// (ldin H, the gradient scale) at the last timestep, else the second half of
+// DXH (ldin 2H, the dh the step after left there, read before this thread
+// overwrites it)
+__global__ void __launch_bounds__(256) k_gen_bwd1(const float* din, long ldin, const uint32_t* __restrict__ gmax,
+                                                  Drop sd, int tm, int v, const float* __restrict__ G,
                                                   const float* __restrict__ h, const float* __restrict__ cc,
                                                   float* __restrict__ dzc, float* __restrict__ dzg,
-                                                  float* __restrict__ DXH, long N, int H, float* __restrict__ bpart) {
+                                                  float* DXH, long N, int H, float* __restrict__ bpart) {
   // grid (column blocks, row slices): column k per thread, the slice's rows in
   // turn; the bias gradients' slice partials sum dzg_u, sum dzc go to the
   // slice's row of bpart ([slices][dbg_r | dbg_u | dbc], summed in a fixed
   // order after the backward: k_sum_rows)
+  sd = drop_resolve(sd);  // (a device-resident key: loaded once)
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= H) return;
   const long per = (N + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(N, r0 + per);
+  const float dsc = gscale(gmax);
+  const bool drop = sd.thr && tm >= 0;
   float sc = 0.f, su = 0.f;
-#pragma unroll 4
+  uint4 w = make_uint4(0u, 0u, 0u, 0u);
+  int gi = (int)(r0 / v), ii = (int)(r0 - (long)gi * v);  // graph and node of the current row
+  if (drop && r0 < r1) w = state_words(sd, gi, ii & ~3, k, tm);
   for (long row = r0; row < r1; ++row) {
+    if (drop && (ii & 3) == 0 && row != r0) w = state_words(sd, gi, ii, k, tm);  // a new row quad
     const long e = row * H + k, g2 = row * 2 * H + H + k;
-    const float u = G[g2], c = cc[e], dl = d[e];
+    float dl = din[row * ldin + k] * dsc;
+    if (drop) dl = drop_apply(sd, u4_get(w, ii & 3), dl);
+    if (++ii == v) { ii = 0; ++gi; }
+    const float u = G[g2], c = cc[e];
     const float zc = dl * (1.0f - u) * (1.0f - c * c), zu = dl * (h[e] - c) * u * (1.0f - u);
     dzc[e] = zc;
     dzg[g2] = zu;

@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) k_embed_bwd_det(EmbArgs a, EmbAcc ea, con
     const long q = e / a.H;
     const int k = (int)(e % a.H);
     const int s = emb_find(a, k);
-    if (s < 0) continue;
+    if (s < 0 || !ea.acc[s]) continue;  // (no accumulator: a segment without a gradient here)
     const EmbSeg& S = a.s[s];
     const uint4 w = dr.thr ? emb_words(dr, q * 4, k) : make_uint4(0u, 0u, 0u, 0u);
     float ss = 0.f;
@@ -226,6 +226,7 @@ __global__ void __launch_bounds__(256) k_embed_fin(EmbArgs a, EmbAcc ea, EmbGrad
   const long r = wv / a.nseg;
   const int s = (int)(wv % a.nseg);
   const EmbSeg& S = a.s[s];
+  if (!ea.acc[s]) return;
   const int id = wi[r * a.ncols + S.column];
   if (id < 0 || id >= S.rows || ea.own[s][id] != emb_owner(a.rows, r, s)) return;
   long long* ar = ea.acc[s] + (long)id * S.width;
@@ -235,6 +236,34 @@ __global__ void __launch_bounds__(256) k_embed_fin(EmbArgs a, EmbAcc ea, EmbGrad
     ar[k] = 0;
   }
   if (lane == 0) ea.own[s][id] = 0;
+}
+
+// One segment's per-lookup gradient rows, as the reference's IndexedSlices
+// holds them (values, indices; chem_tensorflow.py:496-500): rows[r][j] =
+// dropout'(dh0 + dh0_add)[r][offset + j], ids[r] = the looked-up row (-1 out of
+// range); rows r in [rows, cap) are zero with id -1.  The data-parallel step
+// all-gathers them and accumulates the union (ggnn_embed_backward_ws, exact
+// in fixed point) instead of all-reducing the dense table.
+__global__ void __launch_bounds__(256) k_embed_rows(EmbArgs a, int s, const int* __restrict__ wi,
+                                                    const float* __restrict__ dh0, const float* __restrict__ dh0_add,
+                                                    float* __restrict__ rows, int* __restrict__ ids, long cap) {
+  const Drop dr = drop_resolve(a.dr);
+  const EmbSeg& S = a.s[s];
+  const long total = cap * S.width;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / S.width;
+    const int j = (int)(e % S.width), k = S.offset + j;
+    float g = 0.f;
+    int id = -1;
+    if (r < a.rows) {
+      g = dh0[r * a.H + k] + (dh0_add ? dh0_add[r * a.H + k] : 0.f);
+      if (dr.thr) g = drop_apply(dr, u4_get(emb_words(dr, (r >> 2) * 4, k), (int)(r & 3)), g);
+      id = wi[r * a.ncols + S.column];
+      if (id < 0 || id >= S.rows) id = -1;
+    }
+    rows[e] = g;
+    if (j == 0) ids[r] = id;
+  }
 }
 
 // ---------------------------------------------------------------------------

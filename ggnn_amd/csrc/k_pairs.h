@@ -384,6 +384,31 @@ __global__ void k_pair_gather_dx(const int* __restrict__ prow, const unsigned ch
   }
 }
 
+// k_pair_gather_dx and the dL/dbeta tile partials of k_pair_dbeta in one
+// pass (round 5): block = one live pair tile, thread = one 4-column quad of
+// every row of the tile (H / 4 <= 256): dXg[p] = dX of p's node row, and
+// part[tile][k..k+3] = sum over the tile's rows in row order of deg_p dXg[p]
+__global__ void __launch_bounds__(256) k_pair_gather_dx_dbeta(const int* __restrict__ prow,
+                                                              const unsigned char* __restrict__ pmask,
+                                                              const float* __restrict__ pdeg,
+                                                              const float* __restrict__ DXH, float* __restrict__ dXg,
+                                                              float* __restrict__ part, int H) {
+  const int tile = blockIdx.x, k = 4 * threadIdx.x;
+  if (k >= H || !pmask[tile]) return;
+  const long p0 = (long)tile * PAIR_TILE;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int i = 0; i < PAIR_TILE; ++i) {
+    const long p = p0 + i;
+    const int r = prow[p];
+    const float4 x = r >= 0 ? *(const float4*)(DXH + (long)r * 2 * H + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(dXg + p * H + k) = x;
+    const float dg = pdeg[p];
+    s.x += dg * x.x; s.y += dg * x.y; s.z += dg * x.z; s.w += dg * x.w;
+  }
+  if (part) *(float4*)(part + (long)tile * H + k) = s;
+}
+
 // dL/dbeta partials: part[tile][k] = sum over the pair tile's rows (one
 // channel's, padding rows of degree 0) of deg_p dXg[p][k]; grid (column
 // blocks, pair tiles).  The channels' sums over their tiles (and the

@@ -108,20 +108,55 @@ class FlatTrainBuffer:
     copy, and it sums the gradients, the lookup norms and the losses at once.
 
     Each view starts on a 64-float (256-byte) boundary (the library's
-    16-byte vector paths and the MFMA epilogues' stores)."""
+    16-byte vector paths and the MFMA epilogues' stores).
+
+    Layout (round 5): the ``first`` variables (the output heads, whose
+    gradients are final before the propagation backward starts) and the
+    losses, then the other dense variables and the lookup norms, then the
+    ``sparse`` variables (the word embedding table: reduced as IndexedSlices,
+    not all-reduced densely).  ``buckets`` = [(heads + losses), (the rest of
+    the dense part)] as flat slices; ``dense`` = both."""
 
     ALIGN = 64
 
-    def __init__(self, params, n_sq: int, n_loss: int, device=None):
-        sizes = [int(p.numel()) for p in params] + [int(n_sq), int(n_loss)]
-        offs, off = [], 0
-        for n in sizes:
-            offs.append(off)
-            off += -(-n // self.ALIGN) * self.ALIGN
+    def __init__(self, params, n_sq: int, n_loss: int, device=None, first=(), sparse=()):
+        n = len(params)
+        first, sparse = [i for i in first if i not in sparse], list(sparse)
+        rest = [i for i in range(n) if i not in first and i not in sparse]
+        al = lambda k: -(-k // self.ALIGN) * self.ALIGN  # noqa: E731
+        offs, off = [None] * n, 0
+        for i in first:
+            offs[i] = off
+            off += al(int(params[i].numel()))
+        loss_off = off
+        off += al(int(n_loss))
+        self._b0 = off
+        for i in rest:
+            offs[i] = off
+            off += al(int(params[i].numel()))
+        sq_off = off
+        off += al(int(n_sq))
+        self._dense_end = off
+        for i in sparse:
+            offs[i] = off
+            off += al(int(params[i].numel()))
         self.flat = torch.zeros(off, dtype=torch.float32, device=device)
         self.grads = [self.flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
-        self.sq = self.flat[offs[-2]:offs[-2] + n_sq]
-        self.loss = self.flat[offs[-1]:offs[-1] + n_loss]
+        self.sq = self.flat[sq_off:sq_off + n_sq]
+        self.loss = self.flat[loss_off:loss_off + n_loss]
+        self.sparse = tuple(sparse)
+
+    @property
+    def dense(self) -> torch.Tensor:
+        """Everything the all-reduce sums (all but the sparse variables)."""
+        return self.flat[:self._dense_end]
+
+    @property
+    def buckets(self):
+        """(heads + losses, the rest of the dense part): the first is final
+        after the heads' backward, so its reduction can start while the
+        propagation backward runs."""
+        return self.flat[:self._b0], self.flat[self._b0:self._dense_end]
 
     @property
     def nbytes(self) -> int:
@@ -132,13 +167,43 @@ class FlatTrainBuffer:
         self.flat.zero_()
 
 
+class Reducer:
+    """Sums tensors over the ranks of a group (RCCL on GPUs, gloo on CPU).
+    Called as ``r(t)``: a blocking in-place all-reduce.  ``start(t)`` issues
+    it asynchronously (RCCL runs it on its own stream after the work queued
+    so far on the current stream) and returns a handle; ``wait(h)`` makes the
+    current stream wait for it.  ``gather(t)``: all ranks' ``t`` stacked in
+    rank order (all_gather_into_tensor)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = tdist.get_world_size(group)
+
+    def __call__(self, t):
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)
+
+    def start(self, t):
+        return tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    @staticmethod
+    def wait(h):
+        if h is not None:
+            h.wait()
+
+    def gather(self, t):
+        t = t.contiguous()
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        tdist.all_gather_into_tensor(out, t, group=self.group)
+        return out.view((self.world,) + tuple(t.shape))
+
+
 def all_reduce_sum(group=None):
-    """A callable summing a tensor over the ranks of `group` (RCCL on GPUs,
+    """A Reducer summing a tensor over the ranks of `group` (RCCL on GPUs,
     gloo on CPU), or None outside a multi-rank job (a one-rank group counts
     as multi-rank when collectives_at_world_one() is on)."""
     if not _reducing(group):
         return None
-    return lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
+    return Reducer(group)
 
 
 def init_from_env(backend: str | None = None):

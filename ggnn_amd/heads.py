@@ -99,9 +99,36 @@ class EmbeddingFrontEnd:
     def _segs(self, segments, dtables=None):
         arr = (EmbedSegment * len(segments))()
         for i, (t, col) in enumerate(segments):
-            arr[i] = EmbedSegment(t.data_ptr(), None if dtables is None else dtables[i].data_ptr(), t.shape[0],
-                                  t.shape[1], int(col))
+            dt = None if dtables is None or dtables[i] is None else dtables[i].data_ptr()
+            arr[i] = EmbedSegment(t.data_ptr(), dt, t.shape[0], t.shape[1], int(col))
         return arr
+
+    def lookup_rows(self, segments, seg, wi, dh0, keep, seed, rows, ids, dh0_add=None, seed_device=False):
+        """Segment ``seg``'s gradient as IndexedSlices: rows [cap, width] (the
+        per-lookup gradient rows, embedding dropout applied) and ids [cap]
+        (int32, -1 past the batch) -- ggnn_embed_lookup_rows."""
+        b, v, ncols = wi.shape
+        d = _lib.dims(b, v, self.hidden, 1, 1, True, "fp32", seed_device=seed_device)
+        _lib.check(self._lib.ggnn_embed_lookup_rows(ctypes.byref(d), self._segs(segments), len(segments), int(seg),
+                                                    _ptr(wi), ncols, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                    _ptr(dh0.contiguous()),
+                                                    _ptr(None if dh0_add is None else dh0_add.contiguous()),
+                                                    _ptr(rows), _ptr(ids), int(rows.shape[0]), _stream()),
+                   "ggnn_embed_lookup_rows")
+
+    def union_backward(self, table, dtable, rows, ids, sq_out):
+        """The gradient of ``table`` from IndexedSlices (rows [n, width], ids
+        [n]; -1 = none): dtable = the sum of the rows per id in 64-bit fixed
+        point (exact, whatever order -- the same bits on every rank that holds
+        the same slices), sq_out[0] = the sum of the squared rows
+        (ggnn_embed_backward_ws over one segment, keep 1)."""
+        n, w = rows.shape
+        segs = [(table, 0)]
+        d = _lib.dims(int(n), 1, int(w), 1, 1, True, "fp32")
+        _lib.check(self._lib.ggnn_embed_backward_ws(ctypes.byref(d), self._segs(segs, [dtable]), 1,
+                                                    _ptr(ids.contiguous()), 1, 1.0, 0, _ptr(rows.contiguous()),
+                                                    None, _ptr(sq_out), _ptr(self.workspace(segs, rows.device)),
+                                                    _stream()), "ggnn_embed_backward_ws")
 
     def forward(self, segments, wi: torch.Tensor, keep: float = 1.0, seed: int = 0, seed_device: bool = False,
                 out=None) -> torch.Tensor:

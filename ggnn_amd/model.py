@@ -219,6 +219,7 @@ class DenseGGNNChemModel(BtbBatching):
         self._front_end = None
         self._heads = None
         self._flat = None
+        self._rows = None          # the word segment's lookup rows / ids (sparse data-parallel reduction)
         # hipGraph-captured steps by batch shape (graphs.py), least recently
         # used first; bounded by params['hip_graph_cache_mb'] (_evict_graphs)
         self._graphs = OrderedDict()
@@ -423,10 +424,60 @@ class DenseGGNNChemModel(BtbBatching):
         return [(g["weights"][0], g["biases"][0]), (ge["weights"][0], ge["biases"][0])]
 
     def train_buffer(self) -> FlatTrainBuffer:
-        """The flat gradient / lookup-norm / loss buffer of train_step."""
+        """The flat gradient / lookup-norm / loss buffer of train_step.  The
+        output heads' gradients and the losses come first (one bucket, final
+        before the propagation backward); with world_size > 1 and
+        params['sparse_embedding_reduce'] the word table's gradient sits past
+        the dense part: it is reduced as IndexedSlices (_sparse_reduce)."""
         if self._flat is None:
-            self._flat = FlatTrainBuffer(self.trainable_variables(), n_sq=4, n_loss=2, device=self.device)
+            params = self.trainable_variables()
+            ids = {id(p): i for i, p in enumerate(params)}
+            first = [ids[id(t)] for tid in self.params["task_ids"] for hw in self._heads_list(tid) for t in hw]
+            sparse = [ids[id(self.weights["word_embeddings"])]] if self._sparse_reduce_on() else []
+            self._flat = FlatTrainBuffer(params, n_sq=4, n_loss=2, device=self.device, first=first, sparse=sparse)
         return self._flat
+
+    def _sparse_reduce_on(self) -> bool:
+        return self.world_size > 1 and bool(self.params.get("sparse_embedding_reduce", True))
+
+    def _lookup_rows(self):
+        """The word segment's per-lookup gradient rows and ids of this rank's
+        batch (persistent buffers of capacity batch_size * bucket_max_nodes,
+        the same on every rank: what the ranks all-gather)."""
+        if self._rows is None:
+            cap = int(self.params["batch_size"]) * int(self.bucket_max_nodes)
+            w = self.weights["word_embeddings"].shape[1]
+            self._rows = (torch.zeros((cap, w), dtype=torch.float32, device=self.device),
+                          torch.full((cap,), -1, dtype=torch.int32, device=self.device))
+        return self._rows
+
+    def _reduce(self, fl, reducer, started=None) -> None:
+        """The data-parallel reduction of one step's flat buffer: the dense
+        part as (heads + losses) and the rest -- the first bucket possibly
+        started already (``started``: its handle) -- and, with the sparse
+        reduction on, the word table as the union of every rank's lookups:
+        the ranks' (rows, ids) all-gathered, accumulated in fixed point
+        (exact, so the same bits on every rank)."""
+        if fl.sparse and not hasattr(reducer, "gather"):
+            raise TypeError("the sparse word-table reduction needs a dist.Reducer (all_reduce_sum()), "
+                            "or params['sparse_embedding_reduce'] = False")
+        if not hasattr(reducer, "start"):          # a plain callable: one blocking all-reduce
+            reducer(fl.dense)
+        else:
+            b0, b1 = fl.buckets
+            h0 = started if started is not None else reducer.start(b0)
+            reducer(b1)
+            reducer.wait(h0)
+        if fl.sparse:
+            rows, ids = self._lookup_rows()
+            g_rows, g_ids = reducer.gather(rows), reducer.gather(ids)
+            if self._front_end is None:
+                self._front_end = EmbeddingFrontEnd(self.params["hidden_size"])
+            word = self.weights["word_embeddings"]
+            tables = self._front_end_segments()[0]
+            slot = next(i for i, t in enumerate(tables) if t is word)
+            self._front_end.union_backward(word, fl.grads[fl.sparse[0]], g_rows.view(-1, word.shape[1]),
+                                           g_ids.view(-1), fl.sq[slot:slot + 1])
 
     def train_step(self, feed_dict=None, grad_scale=1.0, all_reduce=None, target_count=None, task_id=0):
         """One training step (chem_tensorflow.py:483-506 + run_epoch's
@@ -463,17 +514,22 @@ class DenseGGNNChemModel(BtbBatching):
             target_count = self.placeholders.get("global_target_count")
         fl = self.train_buffer()
         params = self.trainable_variables()
-        self._forward_backward(fl, params, None if target_count is None else float(target_count), task_id)
+        started = []
+        self._forward_backward(fl, params, None if target_count is None else float(target_count), task_id,
+                               reducer=all_reduce, started=started)
         if all_reduce is not None:
-            all_reduce(fl.flat)
+            self._reduce(fl, all_reduce, started[0] if started else None)
         self._apply_gradients(fl, params, grad_scale)
         return fl.loss.sum()
 
     def _empty_train_step(self, all_reduce, grad_scale):
         fl = self.train_buffer()
         fl.zero_()
+        if fl.sparse:                 # no lookups of this rank in the union
+            self._lookup_rows()[0].zero_()
+            self._lookup_rows()[1].fill_(-1)
         if all_reduce is not None:
-            all_reduce(fl.flat)
+            self._reduce(fl, all_reduce)
         self._apply_gradients(fl, self.trainable_variables(), grad_scale)
         return fl.loss.sum()
 
@@ -592,7 +648,7 @@ class DenseGGNNChemModel(BtbBatching):
         self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
         loss = out["loss"]
         if training and not adam:
-            all_reduce(fl.flat)
+            self._reduce(fl, all_reduce)
             self._apply_gradients(fl, params, grad_scale)
             # the union-batch loss: the graph's loss sum was taken before the
             # all-reduce (this rank's share), the eager path's after it
@@ -685,7 +741,7 @@ class DenseGGNNChemModel(BtbBatching):
             raise ValueError("embedding concat width %d > hidden_size %d: the reference's tf.pad fails here "
                              "(SURVEY F7); pass smaller embedding_sizes" % (width, self.params["hidden_size"]))
 
-    def _forward_backward(self, fl, params, target_count, task_id, sf=None):
+    def _forward_backward(self, fl, params, target_count, task_id, sf=None, reducer=None, started=None):
         """The btb loss and every gradient of one staged batch, written into
         the flat buffer ``fl`` (no autograd: each backward of the library
         writes its outputs where the optimizer reads them).  ``sf``: the
@@ -736,6 +792,10 @@ class DenseGGNNChemModel(BtbBatching):
         self.ops["computed_values_edges"] = probs[1].reshape(b, v * oe)
         _, _, dhT, dh0_heads = sf.heads.backward(hT, h0, hl, sf.labels, probs, sf.target_num,
                                                   dws=[gv[id(w)] for w, _ in hl], dbs=[gv[id(bb)] for _, bb in hl])
+        if reducer is not None and started is not None and hasattr(reducer, "start"):
+            # the heads' gradients and the losses are final: their reduction
+            # runs on the collective's stream while the propagation backward runs
+            started.append(reducer.start(fl.buckets[0]))
         # the path's backward (TF autodiff, chem_tensorflow.py:496)
         eg = {"h0": torch.empty_like(h0), "edge_weights": gv[id(W["edge_weights"])],
               "edge_biases": gv[id(beta)] if beta is not None else None,
@@ -743,8 +803,16 @@ class DenseGGNNChemModel(BtbBatching):
               "candidate_kernel": gv[id(gru["candidate_kernel"])], "candidate_bias": gv[id(gru["candidate_bias"])]}
         eng.backward(dhT, eg)
         # the tables' gradients + IndexedSlices norms (h0 feeds the path and the heads)
+        word = self.weights["word_embeddings"]
+        sparse = bool(fl.sparse)
+        dts = [None if (sparse and t is word) else gv[id(t)] for t in tables]
         self._front_end.backward(segs, sf.wi, eg["h0"], keep_e, sf.seeds[0], dh0_add=dh0_heads,
-                                 dtables=[gv[id(t)] for t in tables], sq_out=fl.sq, seed_device=sf.seed_device)
+                                 dtables=dts, sq_out=fl.sq, seed_device=sf.seed_device)
+        if sparse:
+            # the word table as IndexedSlices (rows, ids): all-gathered by _reduce
+            rows, ids = self._lookup_rows()
+            self._front_end.lookup_rows(segs, next(i for i, t in enumerate(tables) if t is word), sf.wi, eg["h0"], keep_e, sf.seeds[0], rows, ids,
+                                        dh0_add=dh0_heads, seed_device=sf.seed_device)
         return probs
 
     def make_optimizer(self) -> ClipAdam:

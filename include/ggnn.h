@@ -313,6 +313,19 @@ int ggnn_embed_backward_ws(const ggnn_dims* d, const ggnn_embed_segment* segs, i
                            const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
                            const float* dh0, const float* dh0_add, float* lookup_sqnorm, void* ws,
                            ggnn_stream_t stream);
+/* (ggnn_embed_backward_ws: a segment whose d_table is NULL gets no gradient
+ * and a zero squared-norm slot.)
+ * Segment `seg`'s gradient as the reference's IndexedSlices (values, indices;
+ * chem_tensorflow.py:496-500): rows [cap][width] = the per-lookup gradient
+ * rows (embedding dropout applied, keep / seed as the forward), ids [cap] =
+ * the looked-up table rows (-1 out of range); rows b*v .. cap-1 are zero with
+ * id -1.  The data-parallel step all-gathers these and accumulates the union
+ * of every rank's lookups with ggnn_embed_backward_ws (keep 1, one segment,
+ * v = 1) instead of all-reducing the dense table. */
+int ggnn_embed_lookup_rows(const ggnn_dims* d, const ggnn_embed_segment* segs, int nseg, int seg,
+                           const int32_t* word_inputs, int ncols, float keep, uint64_t seed,
+                           const float* dh0, const float* dh0_add, float* rows, int32_t* ids,
+                           int64_t cap, ggnn_stream_t stream);
 
 /* Output heads: gated_regression for --pr btb, chem_tensorflow_dense.py:439-516
  * with MLP(2h, o, [], out_layer_dropout_keep_prob) (utils.py:40-84), and the

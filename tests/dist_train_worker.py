@@ -59,7 +59,8 @@ def main():
         flats, losses = [], []
         for _ in range(2):
             loss = mm.train_step(dict(feed), all_reduce=reduce, target_count=tc)
-            flats.append(mm.train_buffer().flat.cpu().numpy().copy())
+            fl = mm.train_buffer()     # (variables in trainable order: the layouts differ with world size)
+            flats.append(torch.cat([g.reshape(-1) for g in fl.grads] + [fl.sq, fl.loss]).cpu().numpy().copy())
             losses.append(float(loss))
         torch.cuda.synchronize()
         return np.concatenate([p.detach().cpu().numpy().ravel() for p in mm.trainable_variables()]), \

@@ -341,3 +341,52 @@ def test_bench_launcher_fails_when_a_rank_fails():
     r = _bench(["--gpus", "2", "--dist-backend", "nccl", "--launch-only"], timeout=120)
     assert r.returncode != 0 and "exited with" in r.stderr, (r.returncode, r.stderr[-2000:])
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as tdist
+    from ggnn_amd.dist import FlatTrainBuffer, all_reduce_sum, init_from_env
+    init_from_env(backend="gloo")
+    g = torch.Generator().manual_seed(100 + rank)
+    params = [torch.zeros(s) for s in ((5, 7), (3,), (40, 6), (9, 2), (2,))]
+    fb = FlatTrainBuffer(params, n_sq=3, n_loss=2, first=(3, 4), sparse=(2,))
+    ff = FlatTrainBuffer(params, n_sq=3, n_loss=2)                        # the round-4 flat layout
+    for a, b in zip(fb.grads + [fb.sq, fb.loss], ff.grads + [ff.sq, ff.loss]):
+        x = torch.randn(a.shape, generator=g)
+        a.copy_(x)
+        b.copy_(x)
+    r = all_reduce_sum()
+    sparse_before = fb.grads[2].clone()
+    h = r.start(fb.buckets[0])       # the heads bucket in flight while "the backward runs"
+    r(fb.buckets[1])
+    r.wait(h)
+    r(ff.flat)
+    dense_equal = all(torch.equal(a, b) for i, (a, b) in enumerate(zip(fb.grads, ff.grads)) if i != 2)
+    ok = [dense_equal, torch.equal(fb.sq, ff.sq), torch.equal(fb.loss, ff.loss),
+          torch.equal(fb.grads[2], sparse_before)]          # the sparse part is not all-reduced
+    gathered = r.gather(torch.full((4,), float(rank)))
+    ok.append(gathered.tolist() == [[0.0] * 4, [1.0] * 4])
+    tdist.barrier()
+    tdist.destroy_process_group()
+    q.put((rank, ok))
+
+
+def test_bucketed_reduction_equals_the_flat_one():
+    """The data-parallel step's reduction as two buckets (heads + losses
+    started asynchronously, then the rest of the dense part) sums exactly what
+    one all-reduce of the round-4 flat buffer sums: bit for bit, two gloo
+    ranks; the sparse region (the word table, reduced as IndexedSlices by the
+    model) is left out of it; gather stacks the ranks in rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get(timeout=5) for _ in range(2))
+    assert got == {0: [True] * 5, 1: [True] * 5}, got

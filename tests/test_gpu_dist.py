@@ -171,6 +171,27 @@ def test_two_rank_captured_step_returns_the_union_loss(tmp_path):
     assert float(d["param_diff"]) == 0.0
 
 
+def test_sparse_word_reduction_matches_the_flat_one(tmp_path):
+    """the data-parallel step's reduction as buckets (the
+    heads' gradients and the losses started asynchronously before the
+    propagation backward) plus the word table as IndexedSlices (the ranks'
+    lookup rows all-gathered and summed in 64-bit fixed point) against the
+    round-4 single all-reduce of the flat buffer, two gloo ranks on the GPU:
+    every dense gradient, the losses and every non-word variable after Adam
+    equal bit for bit; the word gradient and its lookup norm within fp32
+    rounding (the flat path adds each rank's fp32 table, the sparse one
+    converts the exact integer sum once); the sparse result identical on both
+    ranks and equal to the fixed-point sum of the union's lookups."""
+    out = str(tmp_path / "sparse.json")
+    _spawn("dist_sparse_worker.py", [out], tmp_path)
+    with open(out) as f:
+        r = json.load(f)
+    print("sparse word reduction:", r)
+    assert r["sparse_layout"] and r["dense_grads_equal"] and r["loss_equal"] and r["params_equal_but_word"], r
+    assert r["word_grad_rel"] <= 1e-6 and r["word_sq_rel"] <= 1e-5, r
+    assert r["ranks_agree"] and r["union_recomputed_equal"] and r["lookups"] > 0, r
+
+
 def test_rccl_one_rank_group_runs_the_training_collectives(tmp_path):
     """The RCCL path an N-GPU run takes, executed on the test box's one GPU: a
     one-rank "nccl" group made exactly as dist.init_from_env makes it

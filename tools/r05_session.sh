@@ -23,6 +23,16 @@ for l in open('gpurun_out/${TAG}_ab.log'):
         d=json.loads(l); print(d['lib'].split('/')[-1], d['variant'], d['trees'], d['ms_per_step'], {k: v for k, v in d['kernels'].items() if k in ('gru_bwd','wgrad','prop_bwd','state_io','fwd_fused')})
 "
 fi
+if [ -n "$E2E" ]; then
+  # run_epoch at the reference defaults under a kernel + memory-copy trace;
+  # per-batch kernel time, idle split (inside the graph / between steps), copies
+  export TMPDIR=/tmp
+  rm -rf /tmp/${TAG}_e2etrace
+  timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d /tmp/${TAG}_e2etrace -o run -- python3 tools/e2e_profile.py --no-cprofile > gpurun_out/${TAG}_e2etrace.log 2>&1 || { echo E2E_FAILED; tail -20 gpurun_out/${TAG}_e2etrace.log; exit 1; }
+  python3 tools/trace_batch.py "$(find /tmp/${TAG}_e2etrace -name '*kernel_trace.csv' | head -1)" --copies "$(find /tmp/${TAG}_e2etrace -name '*memory_copy_trace.csv' | head -1)" > gpurun_out/${TAG}_e2e_train_batch_kernels.txt 2>&1
+  head -12 gpurun_out/${TAG}_e2e_train_batch_kernels.txt
+  grep -E "inst/s" gpurun_out/${TAG}_e2etrace.log
+fi
 if [ -n "$PROFILE" ]; then
   bash tools/profile_round.sh $TAG || { echo PROFILE_FAILED; tail -20 gpurun_out/${TAG}_*.log; exit 1; }
   grep -h '^{' gpurun_out/${TAG}_trace.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('TRACE LEG', d['value'], d['ms_per_step'], {k: (round(v['avg_launch_ms'],4), round(v['frac'],4)) for k, v in d['roofline']['kernels'].items()})"

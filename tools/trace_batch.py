@@ -1,15 +1,19 @@
 """Per-kernel time per training batch from a rocprofv3 kernel trace of
 tools/e2e_profile.py: the window of the last `--batches` training steps
-(delimited by the optimizer's k_opt_adam launches).
+(delimited by the optimizer's k_opt_adam launches), and where the window's
+idle time sits: between the kernels of one step (inside the replayed graph)
+or between two steps (the host's share: scoring the previous batch, staging
+the next one's inputs, the graph launch), with the H2D copies a
+--memory-copy-trace CSV shows in those gaps.
 
-    python tools/trace_batch.py gpurun_out/<dir>/run_kernel_trace.csv [--batches 102]
+    python tools/trace_batch.py <dir>/run_kernel_trace.csv [--batches 102] [--copies <dir>/run_memory_copy_trace.csv]
 """
 import collections
 import csv
 import sys
 
 
-def main(path, nb=102):
+def main(path, nb=102, copies=None):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "k_opt_adam" in r["Kernel_Name"]]
@@ -24,8 +28,38 @@ def main(path, nb=102):
         tot[k] += d
         cnt[k] += 1
         busy += d
+    # idle time: gaps between consecutive kernels, split at the step boundaries
+    starts = set(i + 1 for i in adam[-(nb + 1):-1])          # first kernel of each step
+    inter, intra, big = 0.0, 0.0, collections.Counter()
+    prev_end = t0
+    for i in range(lo + 1, hi + 1):
+        s, e = int(rows[i]["Start_Timestamp"]), int(rows[i]["End_Timestamp"])
+        gap = max(0, s - prev_end) / 1e3
+        if i in starts:
+            inter += gap
+        else:
+            intra += gap
+            if gap > 5.0:
+                big[rows[i]["Kernel_Name"].split("(")[0][:60]] += gap
+        prev_end = max(prev_end, e)
+    wall = (t1 - t0) / 1e3
     print("window wall %.3f ms/batch, kernels busy %.3f ms/batch, %.1f launches/batch"
-          % ((t1 - t0) / 1e6 / nb, busy / 1e3 / nb, len(win) / nb))
+          % (wall / 1e3 / nb, busy / 1e3 / nb, len(win) / nb))
+    print("idle %.1f us/batch: between steps %.1f us/batch (host: scoring, staging, graph launch), inside the "
+          "step's graph %.1f us/batch (%.2f us per launch boundary)"
+          % ((inter + intra) / nb, inter / nb, intra / nb, intra / max(len(win) - nb, 1)))
+    if big:
+        print("  gaps > 5 us inside the step, before:", ", ".join("%s %.1f us/batch" % (k, v / nb)
+                                                                   for k, v in big.most_common(6)))
+    if copies:
+        cr = list(csv.DictReader(open(copies)))
+        h2d = [r for r in cr if "HOST_TO_DEVICE" in r.get("Direction", "") + r.get("Operation", "")
+               and t0 <= int(r["Start_Timestamp"]) <= t1]
+        d2h = [r for r in cr if "DEVICE_TO_HOST" in r.get("Direction", "") + r.get("Operation", "")
+               and t0 <= int(r["Start_Timestamp"]) <= t1]
+        for name, rs in (("H2D", h2d), ("D2H", d2h)):
+            dur = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rs) / 1e3
+            print("%s copies: %.1f per batch, %.1f us/batch" % (name, len(rs) / nb, dur / nb))
     for k, v in sorted(tot.items(), key=lambda x: -x[1])[:30]:
         print("%8.1f us/batch  %5.1f/batch  avg %6.1f us  %s" % (v / nb, cnt[k] / nb, v / cnt[k], k))
 
@@ -33,4 +67,5 @@ def main(path, nb=102):
 if __name__ == "__main__":
     a = sys.argv[1:]
     nb = int(a[a.index("--batches") + 1]) if "--batches" in a else 102
-    main(a[0], nb)
+    cp = a[a.index("--copies") + 1] if "--copies" in a else None
+    main(a[0], nb, cp)
