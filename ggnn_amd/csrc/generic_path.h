@@ -531,14 +531,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
   const bool dense_ch = (c.flags & GGNN_DENSE_CHANNELS) != 0;
   {
+    // the GRU weight and bias gradients and, in pair mode, dW and dbeta are
+    // stored whole by the fixed-order reductions (§5.1); the dense tiles add
+    // dW over the timesteps and dbeta from the column-sum partials
     Prof p(K_IO, s);
     Zeroer z(s);
-    z.add(dW, C * H * H);
-    z.add(dWg, 4 * H * H);
-    z.add(dbg, 2 * H);
-    z.add(dWc, 2 * H * H);
-    z.add(dbc, H);
-    if (use_bias) z.add(dbeta, C * H);
+    if (!c.sparse) {
+      z.add(dW, C * H * H);
+      if (use_bias) z.add(dbeta, C * H);
+    }
     z.add(P<float>(ws, L.gmax), 1);
   }
   const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);

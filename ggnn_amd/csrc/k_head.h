@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(256) k_embed_bwd_det(EmbArgs a, EmbAcc ea, con
 // the last block sums the squared-norm partials (nblk rows) per slot:
 // 256 threads over contiguous block ranges, then a fixed-order LDS tree
 __global__ void __launch_bounds__(256) k_embed_fin(EmbArgs a, EmbAcc ea, EmbGrad gd, const int* __restrict__ wi,
-                                                   const float* __restrict__ sqp, int nblk, float* __restrict__ sq) {
+                                                   float* __restrict__ sqp, int nblk, float* __restrict__ sq) {
   if (blockIdx.x == gridDim.x - 1) {
     __shared__ float t[256][EMB_MAXSEG + 1];
     const int per = (nblk + 255) / 256, b0 = threadIdx.x * per, b1 = min(nblk, b0 + per);
@@ -204,6 +204,10 @@ __global__ void __launch_bounds__(256) k_embed_fin(EmbArgs a, EmbAcc ea, EmbGrad
       for (int i = 0; i < EMB_MAXSEG; ++i) v[i] += sqp[(long)b * EMB_MAXSEG + i];
 #pragma unroll
     for (int i = 0; i < EMB_MAXSEG; ++i) t[threadIdx.x][i] = v[i];
+    // (the partials are cleared too: the whole workspace is zero after a call)
+    for (int b = b0; b < b1; ++b)
+#pragma unroll
+      for (int i = 0; i < EMB_MAXSEG; ++i) sqp[(long)b * EMB_MAXSEG + i] = 0.f;
     __syncthreads();
     for (int h = 128; h >= 1; h >>= 1) {
       if (threadIdx.x < h)

@@ -145,6 +145,9 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 }
 
 // ===========================================================================
+#ifndef GGNN_PB_WHI
+#define GGNN_PB_WHI 0
+#endif
 // k_prop_bwd: backward of message + aggregation, per channel c
 //   dM_c^T[n][j] = sum_i dX^T[n][i] A_c[i][j]    (K = V; dX^T fragments stay in
 //                                                registers for all channels)
@@ -255,8 +258,13 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
+    // (GGNN_PB_WHI: W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per tile
+    // instead of 3 -- an A/B knob, off: with k_gru_bwd's hi-only weights the
+    // backward's gradients measure up to 8e-4 of the 1e-3 bar, oracle
+    // backward_operand_policy)
+    constexpr bool PWH = SPLIT && GGNN_PB_WHI;
     auto ldb = [&](int ks) {
-      return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
+      return F2{frag_ld(wt, ns, ks, KS, lane), (SPLIT && !PWH) ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
     };
     auto pb = [&](int ks, const F2& w) {
 #pragma unroll
@@ -264,7 +272,8 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(m_hi, off);
         const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-        mma<PREC>(adh[jt], ah, al, w.a, SPLIT ? w.b : w.a);
+        if constexpr (PWH) mma_xb<PREC>(adh[jt], ah, al, w.a);
+        else mma<PREC>(adh[jt], ah, al, w.a, SPLIT ? w.b : w.a);
       }
     };
     b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)

@@ -25,7 +25,7 @@ def main():
                                init_from_env)
     from ggnn_amd.engine import PropagationEngine
     from ggnn_amd.model import DenseGGNNChemModel
-        import ggnn_oracle as O
+    import ggnn_oracle as O
 
     rank, world, local = init_from_env("nccl")
     res = {"backend": tdist.get_backend(), "world": tdist.get_world_size(), "always": collectives_at_world_one()}

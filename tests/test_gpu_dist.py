@@ -29,6 +29,30 @@ def _free_port():
     return p
 
 
+def _adam_agreement(dp_params, full_params, dp_grads, full_grads, what):
+    """Data parallel vs one process on the union batch, Adam at the
+    reference's epsilon 1e-8 (chem_tensorflow.py:494).  The two are not bit
+    for bit: the split-K chunking follows each rank's rows and each rank picks
+    its backward's gradient scale from its own max |dL/dh_T|, so the gradients
+    differ at the rounding level (<= 1e-4 of their max, asserted by the
+    callers); Adam's g / (sqrt(v) + 1e-8) moves every weight by ~lr whatever
+    its gradient's size, so an element whose gradient is itself at that
+    rounding level can move differently by up to ~2 lr per step.  What must
+    agree: every element whose gradient the two runs resolve to 1e-3 relative
+    in every step (the weight gradients' single f16 operands round at ~5e-4)
+    -- there the weights agree to lr x 1e-3 -- most elements are such, and no
+    weight is off by more than 1e-4 (measured 3.2e-6 and 2.9e-5 for the two
+    shapes; lr = 3e-3)."""
+    dg = np.max(np.stack([np.abs(a - b) / np.maximum(np.abs(b), 1e-30) for a, b in zip(dp_grads, full_grads)]), 0)
+    resolved = dg <= 1e-3
+    diff = np.abs(dp_params - full_params)
+    print("%s (Adam epsilon 1e-8): max param diff %.3g overall, %.3g where the gradient is resolved to 1e-3 "
+          "(%d of %d elements)" % (what, diff.max(), diff[resolved].max(), int(resolved.sum()), resolved.size))
+    assert resolved.mean() >= 0.9, resolved.mean()
+    assert diff[resolved].max() <= 3e-6, diff[resolved].max()
+    assert diff.max() <= 1e-4, diff.max()
+
+
 @pytest.mark.parametrize("shape", ["8,64,128,4,3", "4,128,256,8,5"])
 def test_two_rank_engine_step_equals_full_batch(tmp_path, shape):
     out = str(tmp_path / "dp.npz")
@@ -55,11 +79,7 @@ def test_two_rank_engine_step_equals_full_batch(tmp_path, shape):
     step_dp = d["dp_params"] - d["init"]
     step_full = d["full_params"] - d["init"]
     assert np.abs(step_full).max() > 1e-4   # the weights did move
-    diff = np.abs(d["dp_params"] - d["full_params"])
-    print("engine dp vs full (Adam epsilon 1e-8): max param diff %.3g, elements > 1e-6: %d of %d"
-          % (diff.max(), int((diff > 1e-6).sum()), diff.size))
-    assert diff.max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
-    assert np.abs(step_dp - step_full).max() <= 1e-3 * np.abs(step_full).max()
+    _adam_agreement(d["dp_params"], d["full_params"], d["dp_grads"], d["full_grads"], "engine dp vs full")
 
 
 def _spawn(script, args, tmp_path):
@@ -92,10 +112,9 @@ def test_two_rank_btb_train_step_equals_union_batch(tmp_path, hidden):
     np.testing.assert_allclose(d["dp_loss"], d["full_loss"], rtol=1e-5)
     step_full = d["full_params"] - d["init"]
     assert np.abs(step_full).max() > 1e-4
-    diff = np.abs(d["dp_params"] - d["full_params"])
-    print("dp vs union (Adam epsilon 1e-8): max param diff %.3g, elements > 1e-6: %d of %d"
-          % (diff.max(), int((diff > 1e-6).sum()), diff.size))
-    assert diff.max() <= 1e-5 * max(np.abs(d["full_params"]).max(), 1.0)
+    n = d["dp_params"].size
+    _adam_agreement(d["dp_params"], d["full_params"], [f[:n] for f in d["dp_flat"]], [f[:n] for f in d["full_flat"]],
+                    "btb dp vs union")
     # run_epoch with world_size 2: every batch of the single-process schedule
     # ran once (steps summed over the ranks), finite loss, LAS/UAS fractions
     tr_loss, tr_ips, tr_steps, tr_las, tr_uas, va_loss, va_ips, va_steps, va_las, va_uas, n_tr, n_va = d["epoch"]
