@@ -231,7 +231,10 @@ static thread_local int g_gemm_force = 0;
 // ring depth: 2 slots (64 KiB: two workgroups per CU) -- measured 1.4-2x
 // faster than a 4-slot ring (one workgroup per CU) on every probe shape
 // (tools/gemm_ring_probe.py): a second workgroup's MFMAs cover one's prologue,
-// barriers and epilogue better than deeper prefetch does.
+// barriers and epilogue better than deeper prefetch does.  (Round 5: also at
+// the 20-sentence batch's small grids, where one might expect the opposite --
+// 4 slots for grids under 2 workgroups per CU: prop 0.507 -> 0.541 ms, wgrad
+// unchanged; 4 slots for the masked pair dW: wgrad 0.360 -> 0.435 ms.)
 
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
@@ -657,6 +660,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
         SumPlan sp(P<float>(ws, L.SUMS));
         const long S = a.cslots;
         SumJob& q = sp.add(a.cpart, (int)c.b, (int)S, C * S * H, H, C * H, H, S * H, dbeta, dbeta, C * H, 1);
+        q.ugmax = gmax;
         if (!dense_ch) { q.mask = P<const unsigned char>(adj, AL.occ); q.mT = C; q.mC = 1; }
         sp.launch(s);
       }
@@ -685,6 +689,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       // chunks of one channel: slab partials, summed in chunk order (added
       // into dW over the timesteps; stored into this timestep's GW under edge dropout)
       if (chunked) { a.slab = P<float>(ws, L.SLAB); a.sSlab = H * H; }
+      a.ugmax = gmax;  // final values: / S in the epilogue
       if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       if (chunked) slab_reduce(a, (int)C, AL.nch, nullptr, 0, c.ed ? 0 : 1, H * H, s);
@@ -723,6 +728,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // a channel's only chunk stores its dW (zmask 2); several chunks: slab
     // partials summed in chunk order (k_slab_reduce, below)
     a.slab = P<float>(ws, L.SLAB); a.sSlab = H * H;
+    a.ugmax = gmax;
     if (c.ed) {
       a.dr = c.edrop; a.tgroups = c.T;
       // the masks as bits, drawn once per (channel with pairs, timestep, weight)
@@ -760,6 +766,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.sAp = pl.KC * H; a.sBp = pl.KC * ldB; a.K = (int)pl.KC; a.sKp = pl.KC;
       // the z partials in a slab, summed in z order (deterministic)
       a.slab = P<float>(ws, L.SLAB); a.sSlab = H * Nn;
+      a.ugmax = gmax;
       if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       slab_reduce(a, 1, a.Z, nullptr, 0, 0, 0, s);
@@ -777,27 +784,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // rows and of pair mode's per-(timestep, tile) dbeta partials
     SumPlan sp(P<float>(ws, L.SUMS));
     const int nsl = (int)gen_bias_slices(c);
-    sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H);
+    // (these sums, and every weight-gradient product's epilogue, GemmArgs::ugmax,
+    // carry the unscale 1 / S: no separate pass over the gradients)
+    sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
     sp.launch(s);
     if (c.sparse && use_bias) {
       GemmArgs r = gg_args();
       r.slab = P<float>(ws, L.PDB); r.sSlab = H; r.D = dbeta; r.sDm = 0; r.M = 1; r.N = (int)H;
-      slab_reduce_t(r, (int)C, P<const int>(adj, AL.poff), PAIR_TILE, c.T, AL.cap_tiles, s);
+      slab_reduce_t(r, (int)C, P<const int>(adj, AL.poff), PAIR_TILE, c.T, AL.cap_tiles, s, gmax);
     }
-  }
-  {
-    Prof p(K_IO, s);
-    ZeroJobs j;
-    memset(&j, 0, sizeof(j));
-    int nj = 0;
-    auto add = [&](float* p_, long n) { j.p[nj] = p_; j.n[nj++] = n; };
-    add(dW, C * H * H);
-    add(dWg, 4 * H * H);
-    add(dbg, 2 * H);
-    add(dWc, 2 * H * H);
-    add(dbc, H);
-    if (use_bias) add(dbeta, C * H);
-    hipLaunchKernelGGL(k_unscale_multi, dim3(512, nj), dim3(256), 0, s, j, gmax);
   }
   LAUNCHCHK();
   return GGNN_OK;

@@ -291,22 +291,29 @@ struct SumPlan {
   }
 };
 // k_slab_reduce over groups of z (GemmArgs::slab)
+void slab_launch(const SlabRed& r, hipStream_t s) {
+  const long n = (long)r.M * r.N;
+  const bool v4 = r.N % 4 == 0 && r.sSlab % 4 == 0 && (r.zT * r.sSlab) % 4 == 0 && ((uintptr_t)r.slab & 15) == 0;
+  if (v4) hipLaunchKernelGGL(k_slab_reduce<4>, dim3((unsigned)((n / 4 + 255) / 256), (unsigned)r.G), dim3(256), 0, s, r);
+  else hipLaunchKernelGGL(k_slab_reduce<1>, dim3((unsigned)((n + 255) / 256), (unsigned)r.G), dim3(256), 0, s, r);
+}
 void slab_reduce(const GemmArgs& a, int G, int zper, const int* zs, int sole, int add, long sDg, hipStream_t s) {
   SlabRed r;
   memset(&r, 0, sizeof(r));
   r.slab = a.slab; r.sSlab = a.sSlab; r.D = a.D; r.sDg = sDg; r.sDm = a.sDm;
   r.M = a.M; r.N = a.N; r.G = G; r.zper = zper; r.zs = zs; r.zsdiv = 1; r.nt = 1; r.zmask = a.zmask;
   r.sole = sole; r.add = add;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256), (unsigned)G), dim3(256), 0, s, r);
+  slab_launch(r, s);
 }
 // the same over nt per-timestep slab sets of zT z's each, group g's z in
 // [zs[g] / zsdiv, zs[g+1] / zsdiv) (stored, not added)
-void slab_reduce_t(const GemmArgs& a, int G, const int* zs, int zsdiv, int nt, long zT, hipStream_t s) {
+void slab_reduce_t(const GemmArgs& a, int G, const int* zs, int zsdiv, int nt, long zT, hipStream_t s,
+                   const uint32_t* ugmax = nullptr) {
   SlabRed r;
   memset(&r, 0, sizeof(r));
   r.slab = a.slab; r.sSlab = a.sSlab; r.zT = zT; r.D = a.D; r.sDg = (long)a.M * a.N; r.sDm = a.sDm;
-  r.M = a.M; r.N = a.N; r.G = G; r.zs = zs; r.zsdiv = zsdiv; r.nt = nt;
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)(((long)a.M * a.N + 255) / 256), (unsigned)G), dim3(256), 0, s, r);
+  r.M = a.M; r.N = a.N; r.G = G; r.zs = zs; r.zsdiv = zsdiv; r.nt = nt; r.ugmax = ugmax;
+  slab_launch(r, s);
 }
 
 WsL ws_layout(const Cfg& c, bool training) {
@@ -716,22 +723,13 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
                          (long)c.b, gmax);
     // bias gradients: fixed-order sums of the per-(timestep, graph) dbeta and
     // the per-(timestep, workgroup) GRU bias partials
+    // (the sums and k_wgrad_reduce's stores carry the unscale 1 / S: no
+    // separate pass over the gradients)
     SumPlan sp(P<float>(ws, L.sump));
-    sp.rows(P<const float>(ws, L.gbp), c.T, gb_nwg, gb_stride, 3 * H, dbg, dbc, 2 * H);
-    if (use_bias) sp.rows(P<const float>(ws, L.dbp), 1, c.T * c.b, c.T * c.b, (long)c.C * H, dbeta, dbeta, (long)c.C * H);
+    sp.rows(P<const float>(ws, L.gbp), c.T, gb_nwg, gb_stride, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
+    if (use_bias)
+      sp.rows(P<const float>(ws, L.dbp), 1, c.T * c.b, c.T * c.b, (long)c.C * H, dbeta, dbeta, (long)c.C * H).ugmax = gmax;
     sp.launch(s);
-    // weight gradients / S
-    ZeroJobs j;
-    memset(&j, 0, sizeof(j));
-    int nj = 0;
-    auto add = [&](float* p, long n) { j.p[nj] = p; j.n[nj++] = n; };
-    add(dW, (long)c.C * H * H);
-    add(dWg, 4 * H * H);
-    add(dbg, 2 * H);
-    add(dWc, 2 * H * H);
-    add(dbc, H);
-    if (use_bias) add(dbeta, (long)c.C * H);
-    hipLaunchKernelGGL(k_unscale_multi, dim3(512, nj), dim3(256), 0, s, j, gmax);
   }
 
   LAUNCHCHK();
@@ -797,6 +795,7 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   // deterministic reduction over the K chunks (k_wgrad_reduce): the partial
   // tiles live in the workspace
   a.part = P<float>(ws, L.wpart);
+  a.gmax = P<const uint32_t>(ws, L.gmax);  // outputs / S (the backward's gradient scale)
   if (big) {
     const long KC = wp.KC;
     if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
@@ -1073,9 +1072,10 @@ static int adam_impl(const ggnn_adam_tensor* tensors, int count, float learning_
   long maxn = 1;
   for (int i = 0; i < count; ++i) maxn = std::max<long>(maxn, a.t[i].n);
   // scratch holds count * OPT_BLOCKS per-block partial norms
-  const dim3 grid((unsigned)std::min<long>(GGNN_ADAM_SCRATCH_PER_TENSOR, (maxn + 255) / 256), (unsigned)count);
-  hipLaunchKernelGGL(k_opt_sqnorm, grid, dim3(256), 0, s, a, scratch);
-  hipLaunchKernelGGL(k_opt_adam, grid, dim3(256), 0, s, a, (const float*)scratch);
+  const dim3 grid((unsigned)std::min<long>(GGNN_ADAM_SCRATCH_PER_TENSOR, (maxn + OPT_THREADS - 1) / OPT_THREADS),
+                  (unsigned)count);
+  hipLaunchKernelGGL(k_opt_sqnorm, grid, dim3(OPT_THREADS), 0, s, a, scratch);
+  hipLaunchKernelGGL(k_opt_adam, grid, dim3(OPT_THREADS), 0, s, a, (const float*)scratch);
   LAUNCHCHK();
   return GGNN_OK;
 }

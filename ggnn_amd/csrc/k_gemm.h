@@ -105,6 +105,10 @@ struct GemmArgs {
   // afterwards (k_sum_rows)
   float* cpart;
   int cslots;
+  // if set: alpha also carries the backward's gradient unscale 1 / S
+  // (gunscale, ggnn_common.h), so a weight-gradient product stores final
+  // values (S a power of two: the same bits as unscaling afterwards)
+  const uint32_t* ugmax;
 };
 // column-sum partial of the wave whose rows start at row mw and cover nsl
 // 32-row slices (GemmArgs::cpart)
@@ -134,6 +138,7 @@ DEV GemmScales gemm_scales(const GemmArgs& a) {
     if (a.sdev & 2) g.sb = S;
     g.alpha = 1.0f / S;
   }
+  if (a.ugmax) g.alpha *= gunscale(a.ugmax);
   return g;
 }
 
@@ -420,24 +425,50 @@ struct SlabRed {
   const int* zs;
   const unsigned char* zmask;
   int sole, add;
+  const uint32_t* ugmax;  // if set: the sums are multiplied by gunscale (ggnn_common.h)
 };
+// V = 4: four consecutive outputs per thread (N, sDm and sSlab multiples of 4),
+// 16-byte loads; the z's are fetched four at a time (their loads issue
+// together) and added one by one in z order: the same sums as V = 1
+template <int V>
 __global__ void __launch_bounds__(256) k_slab_reduce(SlabRed r) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long e = ((long)blockIdx.x * 256 + threadIdx.x) * V;
   const int g = blockIdx.y;
   if (e >= (long)r.M * r.N) return;
   const int z0 = r.zs ? r.zs[g] / r.zsdiv : g * r.zper, z1 = r.zs ? r.zs[g + 1] / r.zsdiv : (g + 1) * r.zper;
   if (r.sole && z1 - z0 == 1) return;
-  float s = 0.f;
+  float s[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) s[v] = 0.f;
   bool any = false;
   for (int t = 0; t < r.nt; ++t)
-    for (int z = z0; z < z1; ++z) {
-      if (r.zmask && !r.zmask[z]) continue;
-      const float x = r.slab[((long)t * r.zT + z) * r.sSlab + e];
-      s = any ? s + x : x;
-      any = true;
+    for (int z = z0; z < z1; z += 4) {
+      float x[4][V];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int zz = z + u;
+        ok[u] = zz < z1 && (!r.zmask || r.zmask[zz]);
+        const float* src = r.slab + ((long)t * r.zT + (ok[u] ? zz : z0)) * r.sSlab + e;
+        if constexpr (V == 4) {
+          const float4 q = ok[u] ? *(const float4*)src : make_float4(0.f, 0.f, 0.f, 0.f);
+          x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
+        } else {
+          x[u][0] = ok[u] ? *src : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) s[v] = any ? s[v] + x[u][v] : x[u][v];
+          any = true;
+        }
     }
   if (!any && r.add) return;
-  const int m = (int)(e / r.N), n = (int)(e % r.N);
+  const float us = gunscale(r.ugmax);
+  const int m = (int)(e / r.N), n = (int)(e % r.N);  // (V = 4: the four share row m)
   float* d = r.D + (long)g * r.sDg + (long)m * r.sDm + n;
-  *d = r.add ? *d + s : s;
+#pragma unroll
+  for (int v = 0; v < V; ++v) d[v] = r.add ? d[v] + s[v] * us : s[v] * us;
 }

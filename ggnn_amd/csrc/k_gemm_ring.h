@@ -313,19 +313,24 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, slot(u));
-  if constexpr (TGRP && NBUF == 2) {
-    // one call site of the masked banking (the unrolled slot loop inlined it
-    // twice): the slot is picked at run time
+  if constexpr (NBUF == 2) {
+    // one call site of compute (and of the masked banking, which inlined twice
+    // in the unrolled slot loop): the slot is picked at run time.  (The
+    // 128-row tiles without term groups hold 256 VGPRs + 85 AGPRs either way,
+    // one workgroup per CU; forcing two per CU spills 88 B per lane and
+    // measured no faster at the 20-sentence batch or at config 3, round 5)
     for (int it = 0; it < nit; ++it) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
       // (issued ahead of the slice's DMAs: the compiler's wait before their
       // use at the group's end is a vmcnt(0) that also covers those)
-      if (a.mbits && live && gsz > 0 && it % gsz == 0) load_masks(it / gsz);
+      if constexpr (TGRP)
+        if (a.mbits && live && gsz > 0 && it % gsz == 0) load_masks(it / gsz);
       if (it + 1 < nit) stage(it + 1, (it & 1) ? s0 : s1);
       if (live) {
         compute((it & 1) ? s1 : s0);
-        if (gsz > 0 && (it + 1) % gsz == 0) bank_group();
+        if constexpr (TGRP)
+          if (gsz > 0 && (it + 1) % gsz == 0) bank_group();
       }
     }
   } else
@@ -338,6 +343,8 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
         else if (NBUF > 2 && it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
+        if constexpr (TGRP)
+          if (a.mbits && live && gsz > 0 && it % gsz == 0) load_masks(it / gsz);
         if (it + NBUF - 1 < nit) stage(it + NBUF - 1, slot((u + NBUF - 1) % NBUF));
         if (live) {
           compute(slot(u));

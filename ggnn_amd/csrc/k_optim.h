@@ -4,12 +4,18 @@
 //   TF1 AdamOptimizer (chem_tensorflow.py:494-503; tf.compat.v1.train.AdamOptimizer):
 //     m = b1 m + (1-b1) g'' ;  v = b2 v + (1-b2) g''^2
 //     p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps)
-// Two launches: per-tensor sums of squares (fp32 atomics into `sq`), then the
-// elementwise update.  HBM-bound: 4 reads + 3 writes of fp32 per element, as 16-byte pieces.
+// Two launches: per-tensor sums of squares (one partial per block, summed in
+// block order), then the elementwise update.  HBM-bound: 4 reads + 3 writes of
+// fp32 per element, as 16-byte pieces.  Blocks of OPT_THREADS = 1024: a launch
+// has GGNN_ADAM_SCRATCH_PER_TENSOR (256) blocks per tensor, so the largest
+// tensor (the edge weights, the word table) sets its duration, and with
+// 256-thread blocks that tensor's share of the chip was one block, 4 waves, per
+// CU -- too few loads in flight for HBM (2.3-3.5 TB/s measured)
 #pragma once
 #include "ggnn_common.h"
 
 #define GGNN_OPT_MAXT 16
+#define OPT_THREADS 1024
 struct OptTensor {
   float* p;
   const float* g;
@@ -31,8 +37,8 @@ struct OptArgs {
 
 // per-tensor sum of (gscale * g)^2 into sq[tensor]; blockIdx.y = tensor,
 // blockIdx.x strides over its elements (one atomic per block)
-__global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict__ sq) {
-  __shared__ float red[4];
+__global__ void __launch_bounds__(OPT_THREADS) k_opt_sqnorm(OptArgs a, float* __restrict__ sq) {
+  __shared__ float red[OPT_THREADS / 64];
   const OptTensor& T = a.t[blockIdx.y];
   float acc = 0.f;
   if (!T.sqo) {
@@ -55,10 +61,15 @@ __global__ void __launch_bounds__(256) k_opt_sqnorm(OptArgs a, float* __restrict
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   // per-block partial (no atomics, no zeroing): sq[tensor * gridDim.x + block]
-  if (threadIdx.x == 0) sq[blockIdx.y * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < OPT_THREADS / 64; ++w) t += red[w];
+    sq[blockIdx.y * gridDim.x + blockIdx.x] = t;
+  }
 }
 
-__global__ void __launch_bounds__(256) k_opt_adam(OptArgs a, const float* __restrict__ sq) {
+__global__ void __launch_bounds__(OPT_THREADS) k_opt_adam(OptArgs a, const float* __restrict__ sq) {
   const OptTensor& T = a.t[blockIdx.y];
   __shared__ float tot, lr_t;
   if (threadIdx.x == 64) {

@@ -283,6 +283,7 @@ struct SumJob {
   float* out1;
   float* scratch;  // [rcs][E]
   const unsigned char* mask;
+  const uint32_t* ugmax;  // if set: the sums are multiplied by the gradient unscale (gunscale)
   long sT, sW, sC, mT, mC, E, Nc, split;
   int T, nw, rcs, add;  // rcs: row chunks
 };
@@ -324,6 +325,7 @@ __global__ void __launch_bounds__(256) k_sum_rows_fin(SumJobs js) {
   if (e >= J.E) return;
   float s = J.scratch[e];
   for (int rc = 1; rc < J.rcs; ++rc) s += J.scratch[(long)rc * J.E + e];
+  s *= gunscale(J.ugmax);
   float* o = e < J.split ? J.out0 + e : J.out1 + (e - J.split);
   *o = J.add ? *o + s : s;
 }
@@ -694,22 +696,3 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, lon
   }
 }
 
-// ---- divide the backward's outputs by the gradient scale (grouped like
-// k_zero_multi; blockIdx.y = buffer)
-__global__ void __launch_bounds__(256) k_unscale_multi(ZeroJobs a, const uint32_t* __restrict__ gmax) {
-  float* p = a.p[blockIdx.y];
-  const long n = a.n[blockIdx.y];
-  const float sc = gunscale(gmax);
-  const long stride = (long)gridDim.x * 256;
-  long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if ((((unsigned long)p) & 15) == 0) {  // 16-byte pieces, then the tail
-    for (; 4 * i + 3 < n; i += stride) {
-      float4 v = *(float4*)(p + 4 * i);
-      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
-      *(float4*)(p + 4 * i) = v;
-    }
-    for (long k = (n & ~3L) + (long)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) p[k] *= sc;
-  } else {
-    for (; i < n; i += stride) p[i] *= sc;
-  }
-}

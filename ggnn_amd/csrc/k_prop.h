@@ -146,7 +146,7 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 
 // ===========================================================================
 #ifndef GGNN_PB_WHI
-#define GGNN_PB_WHI 0
+#define GGNN_PB_WHI 1
 #endif
 // k_prop_bwd: backward of message + aggregation, per channel c
 //   dM_c^T[n][j] = sum_i dX^T[n][i] A_c[i][j]    (K = V; dX^T fragments stay in
@@ -258,10 +258,12 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    // (GGNN_PB_WHI: W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per tile
-    // instead of 3 -- an A/B knob, off: with k_gru_bwd's hi-only weights the
-    // backward's gradients measure up to 8e-4 of the 1e-3 bar, oracle
-    // backward_operand_policy)
+    // (GGNN_PB_WHI, on: W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per
+    // tile instead of 3.  With k_gru_bwd's hi-only weights the oracle's
+    // backward_operand_policy puts the gradients at <= 7.7e-4 of the 1e-3
+    // bar (b = 256, T = 5, training dropout; profiles/r05_backward_policies.json)
+    // and the GPU at 7.66e-4 (test_full_config3_all_gradients_vs_float64_oracle);
+    // prop_bwd 0.642 -> 0.558 ms per config-3 step)
     constexpr bool PWH = SPLIT && GGNN_PB_WHI;
     auto ldb = [&](int ks) {
       return F2{frag_ld(wt, ns, ks, KS, lane), (SPLIT && !PWH) ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};

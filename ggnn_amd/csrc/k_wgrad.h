@@ -10,8 +10,9 @@
 // over the K chunks (WgArgs::part, round 5): the workgroup stores its partial
 // tile in the accumulator's own register order (16-byte stores, one
 // [TS][TS] block per (tile, chunk)), and k_wgrad_reduce sums the chunks of a
-// tile in chunk order and writes the output once -- the same bits whatever
-// order the workgroups ran in (with part == nullptr: one fp32 atomicAdd per
+// tile in chunk order and writes the output once (times the backward's
+// gradient unscale, WgArgs::gmax) -- the same bits whatever order the
+// workgroups ran in (with part == nullptr: one fp32 atomicAdd per
 // output element and chunk, order-dependent).
 #pragma once
 #include "ggnn_common.h"
@@ -39,6 +40,7 @@ struct WgArgs {
   int nprob, nchunks, KC;
   int H;  // rows of one operand array (wg_off layout); ldP / ldQ hold its N
   float* part;  // [tiles][nchunks][TS * TS] partial tiles (deterministic reduction), or nullptr: atomics
+  const uint32_t* gmax;  // if set: k_wgrad_reduce stores the sums times the gradient unscale (gunscale)
 };
 
 // (problem, batch index, tile origin) of tile `tile` (TS x TS tiles)
@@ -92,10 +94,11 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(WgArgs args) {
   const int m = wt.m0 + (wv / WN) * WMR + i * 32 + acc_row(4 * q, lane >> 5);
   const int nn = wt.n0 + (wv % WN) * WNC + j * 32 + (lane & 31);
   float* o = pr.out + (long)wt.bi * pr.sOb + (long)m * pr.ldO + nn;
-  o[0] = s.x;
-  o[pr.ldO] = s.y;
-  o[2L * pr.ldO] = s.z;
-  o[3L * pr.ldO] = s.w;
+  const float us = gunscale(args.gmax);
+  o[0] = s.x * us;
+  o[pr.ldO] = s.y * us;
+  o[2L * pr.ldO] = s.z * us;
+  o[3L * pr.ldO] = s.w * us;
 }
 
 template <int BK, int PREC>

@@ -59,10 +59,11 @@ def test_split_limbs_on_both_sides_meet_the_max_bar(case):
 
 # ---------------------------------------------------------------------------
 # The fp32-parity BACKWARD's weight limbs (round 5): k_gru_bwd's products
-# dzc Wc^T and dzg Wg^T take the hi limb of the weights only (dz stays a hi/lo
-# pair).  Decided on the oracle (backward_operand_policy) against the 1e-3 bar
-# of max |err| / max |ref| over all seven gradients; the full table is
-# profiles/r05_backward_policies.json (tools/precision_policies.py --backward).
+# dzc Wc^T and dzg Wg^T and k_prop_bwd's dM W_c^T take the hi limb of the
+# weights only (dz and dM stay hi/lo pairs).  Decided on the oracle
+# (backward_operand_policy) against the 1e-3 bar of max |err| / max |ref| over
+# all seven gradients; the full table is profiles/r05_backward_policies.json
+# (tools/precision_policies.py --backward).
 # ---------------------------------------------------------------------------
 BWD_B = 4
 
@@ -91,10 +92,12 @@ def test_backward_policy_exact_equals_oracle_backward(bwd_case):
         assert np.allclose(g[k], ref[k], rtol=1e-10, atol=1e-12), k
 
 
-def test_backward_gru_weight_hi_limb_holds_the_fp32_bar(bwd_case):
+def test_backward_weight_hi_limbs_hold_the_fp32_bar(bwd_case):
     shipped_r4 = _bwd_err(bwd_case, "f16x2", "f16x2", "f16x2", "f16")
-    shipped_r5 = _bwd_err(bwd_case, "f16x2", "f16", "f16x2", "f16")     # k_gru_bwd: Wc^T / Wg^T hi limbs
-    both = _bwd_err(bwd_case, "f16x2", "f16", "f16", "f16")             # + k_prop_bwd's W_c^T (not shipped)
+    gru_only = _bwd_err(bwd_case, "f16x2", "f16", "f16x2", "f16")       # k_gru_bwd: Wc^T / Wg^T hi limbs
+    shipped_r5 = _bwd_err(bwd_case, "f16x2", "f16", "f16", "f16")       # + k_prop_bwd's W_c^T (GGNN_PB_WHI)
     assert shipped_r4 <= 2.5e-4, shipped_r4
-    assert shipped_r5 <= 7e-4, shipped_r5          # measured 5.1e-4 (b = 4), 5.3e-4 (b = 32, dropout)
-    assert shipped_r4 < shipped_r5 < both, (shipped_r4, shipped_r5, both)
+    assert gru_only < shipped_r5, (gru_only, shipped_r5)
+    # the shipped policy: measured 6.4e-4 (b = 4); 7.7e-4 at b = 256 with training
+    # dropout, the worst case of the table (GPU: 7.66e-4)
+    assert shipped_r4 < shipped_r5 <= 9e-4, (shipped_r4, shipped_r5)

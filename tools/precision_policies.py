@@ -78,7 +78,7 @@ def main_backward(b):
                    "dzg, dM operands of the dh / dX chain; gru_wt = Wc^T, Wg^T in k_gru_bwd's products; prop_wt = "
                    "W_c^T in k_prop_bwd's dM W_c^T; wgrad = both operands of the weight-gradient products. Forward "
                    "caches exact, accumulation float64; value = max over the seven gradients of max |err| / "
-                   "max |ref| (the fp32 bar is 1e-3). Round 5 ships gru_wt=f16 (k_gru_bwd hi limbs only).",
+                   "max |ref| (the fp32 bar is 1e-3). Round 5 ships gru_wt=f16, prop_wt=f16 (hi weight limbs in k_gru_bwd and k_prop_bwd).",
            "configs[2]_synthetic": {"shape": "b=%d v=128 hidden=256 C=8 T=5, SURVEY §8d seed 1" % b,
                                     "policies": backward_table(A, h0, w, 5)}}
     At = trees(b, 30, 46, 3)

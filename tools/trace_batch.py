@@ -7,13 +7,14 @@ the next one's inputs, the graph launch), with the H2D copies a
 --memory-copy-trace CSV shows in those gaps.
 
     python tools/trace_batch.py <dir>/run_kernel_trace.csv [--batches 102] [--copies <dir>/run_memory_copy_trace.csv]
+        [--split k_slab_reduce,k_gemm_ring]
 """
 import collections
 import csv
 import sys
 
 
-def main(path, nb=102, copies=None):
+def main(path, nb=102, copies=None, split=()):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "k_opt_adam" in r["Kernel_Name"]]
@@ -28,8 +29,18 @@ def main(path, nb=102, copies=None):
         tot[k] += d
         cnt[k] += 1
         busy += d
-    # idle time: gaps between consecutive kernels, split at the step boundaries
-    starts = set(i + 1 for i in adam[-(nb + 1):-1])          # first kernel of each step
+    # idle time: gaps between consecutive kernels, split at the step boundaries;
+    # a step starts at the first kernel after the optimizer that is not one of
+    # the runtime's copy blits (the previous batch's fetch of the loss and the
+    # heads' probabilities runs as __amd_rocclr_copyBuffer right after Adam):
+    # every gap from Adam's end to that kernel is the host's
+    starts = set()
+    for i in adam[-(nb + 1):-1]:
+        j = i + 1
+        while j < hi and rows[j]["Kernel_Name"].startswith("__amd_rocclr"):
+            starts.add(j)
+            j += 1
+        starts.add(j)
     inter, intra, big = 0.0, 0.0, collections.Counter()
     prev_end = t0
     for i in range(lo + 1, hi + 1):
@@ -62,10 +73,24 @@ def main(path, nb=102, copies=None):
             print("%s copies: %.1f per batch, %.1f us/batch" % (name, len(rs) / nb, dur / nb))
     for k, v in sorted(tot.items(), key=lambda x: -x[1])[:30]:
         print("%8.1f us/batch  %5.1f/batch  avg %6.1f us  %s" % (v / nb, cnt[k] / nb, v / cnt[k], k))
+    # kernels named by --split: per launch grid (the same kernel serves
+    # different products, e.g. k_slab_reduce)
+    for name in split:
+        g, gc = collections.defaultdict(float), collections.Counter()
+        for r in win:
+            if name not in r["Kernel_Name"]:
+                continue
+            key = "%s grid %s x %s" % (r["Kernel_Name"].split("(")[0][:60], r.get("Grid_Size_X", r.get("Grid_Size", "?")),
+                                     r.get("Grid_Size_Y", "1"))
+            g[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            gc[key] += 1
+        for k, v in sorted(g.items(), key=lambda x: -x[1]):
+            print("    %8.1f us/batch  %5.1f/batch  avg %6.1f us  %s" % (v / nb, gc[k] / nb, v / gc[k], k))
 
 
 if __name__ == "__main__":
     a = sys.argv[1:]
     nb = int(a[a.index("--batches") + 1]) if "--batches" in a else 102
     cp = a[a.index("--copies") + 1] if "--copies" in a else None
-    main(a[0], nb, cp)
+    sp = a[a.index("--split") + 1].split(",") if "--split" in a else ()
+    main(a[0], nb, cp, sp)
