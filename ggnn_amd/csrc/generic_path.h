@@ -174,7 +174,7 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
     L.DZG = o; o += 2 * a4 * c.T;
     L.DRH = o; o += a4;
     if (c.ed && !c.sparse) { L.GW = o; o += al((size_t)c.C * H * H * 4); }
-    L.gmax = o; o += al(4);
+    L.gmax = o; o += al(GMAX_BYTES);
     L.SLAB = o; o += al(gen_slab_floats(c) * 4);
     L.GBP = o;  o += al((size_t)c.T * gen_bias_slices(c) * 3 * H * 4);
     if (c.sparse) { L.PDB = o; o += al((size_t)c.T * (c.pcap / PAIR_TILE) * H * 4); }
@@ -538,12 +538,11 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // stored whole by the fixed-order reductions (§5.1); the dense tiles add
     // dW over the timesteps and dbeta from the column-sum partials
     Prof p(K_IO, s);
-    Zeroer z(s);
     if (!c.sparse) {
+      Zeroer z(s);
       z.add(dW, C * H * H);
       if (use_bias) z.add(dbeta, C * H);
     }
-    z.add(P<float>(ws, L.gmax), 1);
   }
   const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
   float* DXH = P<float>(ws, L.DXH);
@@ -551,8 +550,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   float* dM = P<float>(ws, L.M);
   {
     Prof p(K_IO, s);
-    hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(N * H / 4 + 1), 1024)), dim3(256), 0, s, dhT, N * H,
-                       P<uint32_t>(ws, L.gmax));
+    absmax(dhT, N * H, P<uint32_t>(ws, L.gmax), s);
   }
   if (c.sparse) {
     Prof p(K_PROP_BWD, s);

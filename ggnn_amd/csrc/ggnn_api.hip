@@ -291,6 +291,15 @@ struct SumPlan {
   }
 };
 // k_slab_reduce over groups of z (GemmArgs::slab)
+// workspace bytes of the gradient-scale word and k_absmax's block maxima
+constexpr size_t GMAX_BYTES = 256 + ABSMAX_BLOCKS * 4;
+// *gmax = max |x| over n floats as bits (k_absmax + k_absmax_fin; the block
+// maxima 256 bytes past gmax)
+void absmax(const float* x, long n, uint32_t* gmax, hipStream_t s) {
+  float* part = (float*)((char*)gmax + 256);
+  hipLaunchKernelGGL(k_absmax, dim3(ABSMAX_BLOCKS), dim3(ABSMAX_THREADS), 0, s, x, n, part);
+  hipLaunchKernelGGL(k_absmax_fin, dim3(1), dim3(64), 0, s, (const float*)part, ABSMAX_BLOCKS, gmax);
+}
 void slab_launch(const SlabRed& r, hipStream_t s) {
   const long n = (long)r.M * r.N;
   const bool v4 = r.N % 4 == 0 && r.sSlab % 4 == 0 && (r.zT * r.sSlab) % 4 == 0 && ((uintptr_t)r.slab & 15) == 0;
@@ -349,7 +358,7 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.dMT = o;  o += C * L.nhw * T;
     if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
     L.dbp = o; o += al(T * (size_t)c.b * C * H * 4);    // per-(timestep, graph) dL/dbeta partials
-    L.gmax = o; o += al(4);                               // max |dL/dh_T| (gradient scale, ggnn_common.h)
+    L.gmax = o; o += al(GMAX_BYTES);                      // max |dL/dh_T| (gradient scale, ggnn_common.h) + k_absmax partials
     if (H >= 128) {                                       // deterministic K-chunk reduction of the weight gradients
       const WgPlan w = wg_plan(c);
       L.wpart = o; o += al((size_t)w.tiles * w.nchunks * w.TS * w.TS * 4);
@@ -663,21 +672,15 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
 
-  {
-    // (the weight and bias gradients need no clearing: k_wgrad_reduce,
-    // k_edge_mask_reduce and k_sum_rows store every element once)
-    Prof p(K_IO, s);
-    Zeroer z(s);
-    z.add(P<float>(ws, L.gmax), 1);
-  }
+  // (the weight and bias gradients need no clearing: k_wgrad_reduce,
+  // k_edge_mask_reduce and k_sum_rows store every element once)
   // gradient scale: the backward runs on S * dL/dh_T, S = 2^-floor(log2 max|dL/dh_T|),
   // and divides its outputs by S (ggnn_common.h gscale): loss-normalised
   // gradients (~1/b) stay inside the f16 limbs' normal range
   const uint32_t* gmax = P<const uint32_t>(ws, L.gmax);
   {
     Prof p(K_IO, s);
-    const long n = (long)c.b * c.vin * H;
-    hipLaunchKernelGGL(k_absmax, dim3(std::min(grid1d(n / 4 + 1), 1024)), dim3(256), 0, s, dhT, n, P<uint32_t>(ws, L.gmax));
+    absmax(dhT, (long)c.b * c.vin * H, P<uint32_t>(ws, L.gmax), s);
   }
   float* dA = P<float>(ws, L.dA);
   float* dB = P<float>(ws, L.dB);

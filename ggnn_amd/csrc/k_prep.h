@@ -304,13 +304,19 @@ __global__ void __launch_bounds__(256) k_sum_rows(SumJobs js) {
   const long r0 = rc * per, r1 = min(rows, r0 + per);
   __shared__ float red[4][64];
   float s = 0.f;
-  if (e < J.E) {
+  if (e < J.E && r0 + w < r1) {
     const long ec = e / J.Nc, eo = ec * J.sC + e % J.Nc;
+    // row r = t * nw + ww walked incrementally (a 64-bit division per row
+    // bounded the kernel: 16 us for 26 MB at config 3, round 5)
+    int t = (int)((r0 + w) / J.nw), ww = (int)((r0 + w) % J.nw);
 #pragma unroll 4
     for (long r = r0 + w; r < r1; r += 4) {
-      const long t = r / J.nw, ww = r % J.nw;
-      if (J.mask && !J.mask[t * J.mT + ec * J.mC]) continue;
-      s += J.part[t * J.sT + ww * J.sW + eo];
+      if (!J.mask || J.mask[t * J.mT + ec * J.mC]) s += J.part[t * J.sT + ww * J.sW + eo];
+      ww += 4;
+      while (ww >= J.nw) {
+        ww -= J.nw;
+        ++t;
+      }
     }
   }
   red[w][lane] = s;
@@ -324,6 +330,7 @@ __global__ void __launch_bounds__(256) k_sum_rows_fin(SumJobs js) {
   const long e = (long)(blockIdx.x - js.fx[ji]) * 256 + threadIdx.x;
   if (e >= J.E) return;
   float s = J.scratch[e];
+#pragma unroll 8
   for (int rc = 1; rc < J.rcs; ++rc) s += J.scratch[(long)rc * J.E + e];
   s *= gunscale(J.ugmax);
   float* o = e < J.split ? J.out0 + e : J.out1 + (e - J.split);
@@ -660,12 +667,18 @@ __global__ void __launch_bounds__(256) k_zero_multi(ZeroJobs a) {
   }
 }
 
-// ---- max |x| over n floats into *gmax (as bits; *gmax zeroed beforehand):
-// the backward's gradient scale (gscale, ggnn_common.h)
-__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, long n, uint32_t* __restrict__ gmax) {
+// ---- max |x| over n floats into *gmax (as bits): the backward's gradient
+// scale (gscale, ggnn_common.h).  Two launches, no atomics: ABSMAX_BLOCKS
+// blocks store their maxima, one block takes the max of those.  (One
+// same-address atomicMax per block -- device-scope atomics on one line are
+// serialised past the XCDs' L2s -- plus the zeroing of *gmax took 21.5 + 4.2
+// us per config-3 backward for 33 MB, round 5.)
+#define ABSMAX_BLOCKS 256
+#define ABSMAX_THREADS 1024
+__global__ void __launch_bounds__(ABSMAX_THREADS) k_absmax(const float* __restrict__ x, long n, float* __restrict__ part) {
   float m = 0.0f;
-  const long stride = (long)gridDim.x * 256;
-  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long stride = (long)gridDim.x * ABSMAX_THREADS;
+  long i = (long)blockIdx.x * ABSMAX_THREADS + threadIdx.x;
   if ((((unsigned long)x) & 15) == 0) {
     // four independent 16-byte loads in flight per thread, then the rest
     for (; 4 * (i + 3 * stride) + 3 < n; i += 4 * stride) {
@@ -680,19 +693,27 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, lon
       const float4 a = *(const float4*)(x + 4 * i);
       m = fmaxf(m, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
     }
-    for (long k = (n & ~3L) + (long)blockIdx.x * 256 + threadIdx.x; k < n; k += stride) m = fmaxf(m, fabsf(x[k]));
+    for (long k = (n & ~3L) + (long)blockIdx.x * ABSMAX_THREADS + threadIdx.x; k < n; k += stride) m = fmaxf(m, fabsf(x[k]));
   } else {
     for (; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
   }
   // (fmaxf drops NaN; an inf stays inf and disables the scaling)
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  __shared__ float wm[4];
+  __shared__ float wm[ABSMAX_THREADS / 64];
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    atomicMax(gmax, __float_as_uint(m));
+#pragma unroll
+    for (int w = 1; w < ABSMAX_THREADS / 64; ++w) m = fmaxf(m, wm[w]);
+    part[blockIdx.x] = m;
   }
+}
+__global__ void __launch_bounds__(64) k_absmax_fin(const float* __restrict__ part, int nb, uint32_t* __restrict__ gmax) {
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < nb; i += 64) m = fmaxf(m, part[i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (threadIdx.x == 0) *gmax = __float_as_uint(m);
 }
 
