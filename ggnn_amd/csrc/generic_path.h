@@ -423,6 +423,9 @@ int gen_pairs_product(const Cfg& c, const GenAdjL& AL, const void* adj, const fl
   z.D = D; z.sDz = PAIR_TILE * H; z.sDm = H; z.sDn = 1;
   z.tl = P<const int>(adj, AL.ptile); z.ts = 2; z.zmask = P<const unsigned char>(adj, AL.pmask);
   z.Z = AL.cap_tiles; z.M = PAIR_TILE; z.N = (int)H; z.K = (int)H;
+#ifdef GGNN_TS
+  z.tsprobe = wt ? 4 : 3;
+#endif
   return gg_launch<PREC>(z, false, true, wt, kind, s);
 }
 // channel lists of the staged batch (per graph, per channel); rebuilt by every
@@ -727,6 +730,9 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     // partials summed in chunk order (k_slab_reduce, below)
     a.slab = P<float>(ws, L.SLAB); a.sSlab = H * H;
     a.ugmax = gmax;
+#ifdef GGNN_TS
+    a.tsprobe = 1;
+#endif
     if (c.ed) {
       a.dr = c.edrop; a.tgroups = c.T;
       // the masks as bits, drawn once per (channel with pairs, timestep, weight)
@@ -765,6 +771,9 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       // the z partials in a slab, summed in z order (deterministic)
       a.slab = P<float>(ws, L.SLAB); a.sSlab = H * Nn;
       a.ugmax = gmax;
+#ifdef GGNN_TS
+      a.tsprobe = out == dWc ? 2 : 0;
+#endif
       if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;
       Prof p(K_WGRAD, s);
       slab_reduce(a, 1, a.Z, nullptr, 0, 0, 0, s);

@@ -910,6 +910,10 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
 extern "C" {
 #ifdef GGNN_TS
 int ggnn_dbg_ts(void* host) { return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ts), sizeof(g_ts)); }
+int ggnn_dbg_ts_clear(void) {
+  static unsigned long long zero[sizeof(g_ts) / 8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ts), zero, sizeof(g_ts));
+}
 #endif
 
 int ggnn_version(void) { return 4; }

@@ -41,8 +41,10 @@ typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 #ifdef GGNN_TS
 __device__ unsigned long long g_ts[4][2048 * 8];
 #define TSMARK(k, i) do { if (threadIdx.x == 0) g_ts[k][blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TSVAL(k, i, v) do { if (threadIdx.x == 0) g_ts[k][blockIdx.x * 8 + (i)] = (unsigned long long)(v); } while (0)
 #else
 #define TSMARK(k, i) do {} while (0)
+#define TSVAL(k, i, v) do {} while (0)
 #endif
 
 enum { PREC_BF16 = 0, PREC_F16 = 1, PREC_SPLIT = 2 };

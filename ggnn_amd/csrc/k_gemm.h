@@ -109,6 +109,9 @@ struct GemmArgs {
   // (gunscale, ggnn_common.h), so a weight-gradient product stores final
   // values (S a power of two: the same bits as unscaling afterwards)
   const uint32_t* ugmax;
+  // -DGGNN_TS experiment builds: k + 1 = record this launch's per-workgroup
+  // phase stamps in g_ts[k] (tools/ts_probe_generic.py); 0 = none
+  int tsprobe;
 };
 // column-sum partial of the wave whose rows start at row mw and cover nsl
 // 32-row slices (GemmArgs::cpart)

@@ -116,6 +116,8 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   const int wm = w % WMW, wn = w / WMW;
   int z, mt, ntile;
   ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  const int tsk = a.tsprobe - 1;
+  if (tsk >= 0) TSMARK(tsk, 0);
   if (z >= a.Z) return;
   // zmask[z]: 0 skip z, 1 live, 2 live and the only z writing its outputs
   // (GG_ATOMIC then stores: the pair dW chunk that is its channel's only one)
@@ -310,6 +312,11 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   };
 
   // ---- the ring: slices it+1, it+2 stay in flight while slice it is consumed
+  if (tsk >= 0) {
+    TSMARK(tsk, 1);
+    TSVAL(tsk, 5, nit);
+    TSVAL(tsk, 6, z);
+  }
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, slot(u));
@@ -354,12 +361,78 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
       }
     }
   }
+  if (tsk >= 0) TSMARK(tsk, 2);
+  const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
+  const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
+  // Plain stores (GG_STORE, a sole chunk, a split-K slab) with no activation,
+  // dropout, E factor or column split take a lean epilogue: the general one
+  // below unrolls every option's code for each of the 64 accumulator elements
+  // (~11k instructions with the Philox draws), and walking it cost 14-16 us per
+  // workgroup -- more than the K loop at the 20-sentence batch's split-K and
+  // pair products (round 5, tools/ts_probe_generic.py).  Row-major outputs
+  // (unit column stride, 16-byte aligned rows) go through LDS: each wave
+  // parks its tile row-major (XOR-swizzled 16-byte chunks) and stores whole
+  // 16-byte row pieces, a quarter of the store instructions -- a workgroup's
+  // scalar stores of a 128 x 128 tile took ~8 us, one outstanding-store
+  // window after another.  Same arithmetic, same bits.
+  const bool to_slab = a.mode == GG_ATOMIC && !sole;
+  const bool lean = !a.E && a.epi == GG_EPI_NONE && (TGRP || !dr.thr) && !a.Nsplit &&
+                    (a.mode == GG_STORE || sole || (to_slab && a.slab));
+  if (lean) {
+    float* const Db = to_slab ? a.slab + (long)z * a.sSlab : a.D + dbase;
+    const long sm = to_slab ? (long)a.N : a.sDm, sn = to_slab ? 1 : a.sDn;
+    constexpr int WR = AM * 32, WC = AN * 32, C4 = WC / 4;  // a wave's tile, its 16-byte chunks per row
+    // (the parked tiles take both ring slots at 128-row tiles, one at 32)
+    constexpr bool PARK_OK = BMT == 128 ? SB >= 2 * WR * WC * 4 : SB >= 4 * WR * WC * 4;
+    const bool vec = PARK_OK && sn == 1 && a.N % 4 == 0 && sm % 4 == 0 && ((uintptr_t)Db & 15) == 0;
+    if (vec) __syncthreads();  // every wave is done with the ring: its slots take the tiles
+    if (!live) return;
+    float* const park = BMT == 128 ? (float*)(w < 2 ? s0 : s1) + (w & 1) * WR * WC : (float*)s0 + w * WR * WC;
+    auto pk_off = [&](int row, int col) { return row * WC + ((((col >> 2) ^ row) & (C4 - 1)) << 2) + (col & 3); };
+#pragma unroll
+    for (int j = 0; j < AN; ++j) {
+      const int n = n0 + wn * AN * 32 + 32 * j + l32;
+      float cs = 0.f;
+      if (n < a.N) {
+        const float bn = bias ? bias[n] : 0.f;
+        float* const Dc = Db + (long)n * sn;
+#pragma unroll
+        for (int i = 0; i < AM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = 32 * i + acc_row(r, hh), m = m0 + wm * AM * 32 + rl;
+            const float x = gs.alpha * (TGRP ? bank[i][j][r] : acc[i][j][r]) + bn;
+            if (m < a.M) cs += x;
+            if (vec) park[pk_off(rl, 32 * j + l32)] = x;
+            else if (m < a.M) Dc[(long)m * sm] = x;
+          }
+      }
+      if (a.csum) {
+        cs += __shfl_xor(cs, 32);
+        if (hh == 0 && n < a.N) {
+          if (a.cpart) csum_part(a, z, m0 + wm * AM * 32, AM, n, cs);
+          else atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);
+        }
+      }
+    }
+    if (vec) {
+      __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, in order)
+      const int mw0 = m0 + wm * AM * 32, nw0 = n0 + wn * AN * 32;
+#pragma unroll
+      for (int q = 0; q < WR * C4 / 64; ++q) {
+        const int idx = q * 64 + lane, rl = idx / C4, c4 = idx % C4;
+        const int m = mw0 + rl, n = nw0 + 4 * c4;
+        if (m < a.M && n < a.N)
+          *(float4*)(Db + (long)m * sm + n) = *(const float4*)(park + rl * WC + (((c4 ^ rl) & (C4 - 1)) << 2));
+      }
+    }
+    if (tsk >= 0) TSMARK(tsk, 3);
+    return;
+  }
   if (!live) return;  // nothing of this wave's to store (no barrier follows)
 
   // ---- epilogue (as k_gemm)
   constexpr bool EPI_PRE = !TGRP && !A16;  // (masked dW products: atomics only; adjacency products: kept at 3 workgroups per CU)
-  const long dbase = (long)z * a.sDz + (long)zp * a.sDp + (long)zq * a.sDq;
-  const float* bias = a.bias ? a.bias + (long)zp * a.sbp + (long)zq * a.sbq : nullptr;
 #pragma unroll
   for (int j = 0; j < AN; ++j) {
     const int n = n0 + wn * AN * 32 + 32 * j + l32;
@@ -419,6 +492,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
       }
     }
   }
+  if (tsk >= 0) TSMARK(tsk, 3);
 }
 
 // ---- k_gemm_ks: 32-row tiles whose K slices are split over the waves (same
@@ -455,6 +529,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
   const int wn = w % WN, wk = w / WN;
   int z, mt, ntile;
   ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  const int tsk = a.tsprobe - 1;
+  if (tsk >= 0) TSMARK(tsk, 0);
   if (z >= a.Z) return;
   if (a.zmask && !a.zmask[z]) return;
   const int n0 = ntile * 32 * WN + 32 * wn, m0 = mt * 32;  // n0: this wave's column block

@@ -27,9 +27,12 @@
 #include "ggnn_common.h"
 
 #define PAIR_TILE 32   // rows per product tile (the ring kernel's 32-row variant)
-// tiles per split-K term list of the dW product (512 rows; 4 and 8 measured
-// slower: more chunks, more atomics)
-#define PAIR_CHUNK 16
+// tiles per split-K term list of the dW product (128 rows).  16 (512 rows) was
+// the atomic-era choice (4 and 8 meant more chunks, more atomics); with slab
+// partials a shorter list caps the longest workgroup's walk instead (a
+// 20-sentence batch's busiest channel: 64 -> 16 slices; with the ring's lean
+// epilogue the product went 159 -> 105 us, tools/ts_probe_generic.py, round 5)
+#define PAIR_CHUNK 4
 
 // S1: in-degree per (channel, node row) from the staged 16-bit rows (0/1
 // limbs: nonzero bits <=> 1); one block per (graph, channel) tile, a wave per row
