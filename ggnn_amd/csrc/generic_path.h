@@ -74,7 +74,6 @@ struct GenWsL {
   // timestep, so dW_c = sum_t mask_t (Y_t^T dXg_t) runs as ONE product after
   // the timestep loop; WTL: its term lists, every timestep's tiles of a chunk)
   size_t WTL, pslice;
-  size_t MB;  // edge-dropout keep bits of every timestep (k_edge_bits; pair mode, training)
   // deterministic reductions (round 5): split-K slabs of the weight-gradient
   // products (GemmArgs::slab), the element-wise kernels' bias partials
   // [T][slices][dbg_r | dbg_u | dbc], pair mode's per-tile dbeta partials
@@ -162,7 +161,6 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
       L.PDX = o; o += al((size_t)slices * L.pslice * 4);
       const size_t zw = (c.pcap / PAIR_TILE) / PAIR_CHUNK + c.C;
       L.WTL = o; o += al(zw * (1 + (size_t)c.T * PAIR_CHUNK) * 4);
-      if (c.ed) { L.MB = o; o += al((size_t)c.T * c.C * H * ((H + 31) / 32) * 4); }
     }
   } else {
     L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
@@ -308,7 +306,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else if (AKC && !BKC) GGR(false, true, false);
     else if (AKC && BKC) GGR(false, true, true);
     else if (!AKC && !BKC && a.tgroups > 1) {
-      if (a.dr.thr && !a.mbits) return fail(GGNN_EINVAL, "k_gemm_ring: masked term groups need the mask bits (k_edge_bits)");
+      if (a.dr.thr && !a.mbits) return fail(GGNN_EINVAL, "k_gemm_ring: masked term groups need the mask bits (the pack's)");
       // (a 4-slot ring, three slices in flight at one workgroup per CU, measured
       // slower for the weight-gradient products: 1.37 -> 1.72 ms at the
       // reference configuration)
@@ -735,15 +733,10 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
 #endif
     if (c.ed) {
       a.dr = c.edrop; a.tgroups = c.T;
-      // the masks as bits, drawn once per (channel with pairs, timestep, weight)
-      // instead of in every dW tile's epilogue at every timestep
+      // the masks as bits: written by the pack beside its masked copies
+      // (ggnn_pack_weights*, one Philox draw per weight and timestep for both)
       const int w32 = (int)((H + 31) / 32);
-      uint32_t* mb = P<uint32_t>(ws, L.MB);
-      {
-        Prof p(K_WGRAD, s);
-        hipLaunchKernelGGL(k_edge_bits, dim3(grid1d((long)c.T * C * H * w32)), dim3(256), 0, s, c.edrop,
-                           P<const int>(adj, AL.pcnt), (int)C, (int)H, c.T, w32, mb);
-      }
+      const uint32_t* mb = P<const uint32_t>(pack, PL.gb(0));
       a.mbits = mb; a.mbw = w32; a.mbC = (int)C;
     }
     if (int e = gg_launch<WPREC>(a, false, false, false, K_WGRAD, s)) return e;

@@ -162,10 +162,12 @@ struct PackL {
   size_t Wf, WT, beta, Wg, WgT, Wc, WcT, bg, bc, szW;
   size_t gW, gszW, gWg, gWc, chocc, total;  // general path: fp32 W (per timestep under edge dropout), Wg, Wc;
                                             // chocc: the batch's channel occupancy (ggnn_pack_weights_batch)
+  size_t gbits, gszB;  // edge dropout: the masked copies' keep bits per timestep (the pair dW product's mbits)
   long loW, loWg, loWc;  // element offset of the lo part from the hi part
   size_t wf(int t) const { return Wf + (size_t)t * szW; }
   size_t wt(int t) const { return WT + (size_t)t * szW; }
   size_t gw(int t) const { return gW + (size_t)t * gszW; }
+  size_t gb(int t) const { return gbits + (size_t)t * gszB; }
 };
 PackL pack_layout(const Cfg& c) {
   PackL L;
@@ -194,6 +196,10 @@ PackL pack_layout(const Cfg& c) {
   L.gWg = o;  o += al(4 * H * H * 4);
   L.gWc = o;  o += al(2 * H * H * 4);
   L.chocc = o; o += al(c.C);
+  if (c.ed) {
+    L.gszB = (size_t)c.C * H * ((H + 31) / 32) * 4;
+    L.gbits = o; o += al(L.gszB * c.T);
+  }
   L.total = o;
   return L;
 }
@@ -863,17 +869,19 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
     a.blk_begin[a.count++] = nb;
     nb += (int)((J.total + 255) / 256);
   };
-  auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0) {
+  auto copy = [&](const float* S, float* out, long n, int mode = 1, int t = 0, int drop = 0, uint32_t* bits = nullptr) {
     if (a.count == PACK_MAXJ) flush();
     PackJob& J = a.j[a.count];
     // mode 2: 16-byte pieces when H % 4 == 0 and both ends are 16-byte aligned
-    // (masked: one thread per 4-row quad of 4 columns); else one thread per
-    // element, or per 4-row quad of a column when masked (a partial last quad
-    // when H % 4 != 0)
+    // (masked: one thread per 32-row block of 4 columns); else one thread per
+    // element, or per 32-row block of a column when masked (a partial last
+    // quad when H % 4 != 0)
     const int vec = mode == 2 && H % 4 == 0 && !(((uintptr_t)S | (uintptr_t)out) & 15);
-    if (mode == 2 && vec) n = drop ? (long)c.C * (H / 4) * (H / 4) : n / 4;
-    else if (mode == 2 && drop) n = (long)c.C * ((H + 3) / 4) * H;
+    const long w32 = (H + 31) / 32;
+    if (mode == 2 && vec) n = drop ? (long)c.C * w32 * (H / 4) : n / 4;
+    else if (mode == 2 && drop) n = (long)c.C * w32 * H;
     J.S = S; J.out = (u16*)out; J.total = n; J.copy = mode; J.K = H; J.t = t; J.drop = drop; J.trans = vec;
+    J.bits = drop ? bits : nullptr;
     a.blk_begin[a.count++] = nb;
     nb += (int)((n + 255) / 256);
   };
@@ -894,7 +902,8 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
   // the specialised kernels: a pack is made with b = v = 1 dims and may serve a
   // later general-path batch (v > 128).  Measured cost at config 3: 3.5 MB of
   // copies, the whole pack launch 0.013 ms per step (profiles/r03b_bench.json)
-  for (int t = 0; t < (c.ed ? c.T : 1); ++t) copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed);
+  for (int t = 0; t < (c.ed ? c.T : 1); ++t)
+    copy(W, P<float>(pack, L.gw(t)), (long)c.C * H * H, 2, t, c.ed, c.ed ? P<uint32_t>(pack, L.gb(t)) : nullptr);
   copy(Wg, P<float>(pack, L.gWg), 4L * H * H);
   copy(Wc, P<float>(pack, L.gWc), 2L * H * H);
   flush();

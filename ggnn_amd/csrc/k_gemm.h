@@ -87,7 +87,8 @@ struct GemmArgs {
   // timestep k (not drop_t) at each group's end and banked, so one launch sums
   // mask_t-weighted products over t (the pair-mode dW over all timesteps)
   int tgroups;
-  // TGRP with dropout: the keep masks as bits (k_edge_bits; required, the
+  // TGRP with dropout: the keep masks as bits (written by the pack beside its
+  // masked W copies, PackJob::bits; required, the
   // kernel draws no Philox words): word ((t*C + zp)*N + n)*mbw + m/32, bit m%32
   // (mbC = C)
   const uint32_t* mbits;

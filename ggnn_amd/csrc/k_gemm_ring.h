@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   };
 
   // ---- TGRP: group tg (timestep tg) done: bank += mask_tg * acc, acc = 0.
-  // The group's mask words (GemmArgs::mbits, drawn by k_edge_bits) are loaded
+  // The group's mask words (GemmArgs::mbits, the pack's keep bits) are loaded
   // at its first slice (mw: this lane's 32-row word per accumulator tile);
   // drawing Philox words here, per 128 x 128 tile and timestep, was most of the
   // kernel's issue at small batches and spilled at 2 waves per EU

@@ -169,33 +169,6 @@ __global__ void k_pair_fill(const u16* __restrict__ degc, int* __restrict__ pidx
   }
 }
 
-// B4b: the edge-dropout keep masks of every timestep as bits, for the masked
-// dW product (GemmArgs::mbits): mb[((t*C + c)*H + j)*W32 + w] bit b = keep of
-// W_c[i = 32w + b][j] at timestep t (the Philox block (i>>2, j, c, t), word
-// i&3: the masks of ggnn_pack_weights' copies).  Channels without pairs in
-// the batch (pcnt[c] == 0) are skipped: no dW tile reads them.  One thread
-// per word (8 Philox blocks).
-__global__ void __launch_bounds__(256) k_edge_bits(Drop dr, const int* __restrict__ pcnt, int C, int H, int T,
-                                                   int W32, uint32_t* __restrict__ mb) {
-  dr = drop_resolve(dr);  // (a device-resident key: loaded once)
-  const long total = (long)T * C * H * W32;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int w = (int)(e % W32);
-    const long r = e / W32;
-    const int j = (int)(r % H), c = (int)((r / H) % C), t = (int)(r / ((long)H * C));
-    if (!pcnt[c]) continue;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int i = 32 * w + 4 * q;
-      if (i >= H) break;
-      const uint4 x = edge_words(dr, c, i, j, t);
-      bits |= (uint32_t)(x.x < dr.thr) << (4 * q) | (uint32_t)(x.y < dr.thr) << (4 * q + 1) |
-              (uint32_t)(x.z < dr.thr) << (4 * q + 2) | (uint32_t)(x.w < dr.thr) << (4 * q + 3);
-    }
-    mb[e] = bits;
-  }
-}
 
 // B5: the dW product's term lists over all T timesteps: chunk z's tiles
 // (wtl[z*(1+PAIR_CHUNK)]) repeated per timestep as q = t * cap_tiles + tile,

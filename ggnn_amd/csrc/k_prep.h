@@ -493,6 +493,10 @@ __global__ void __launch_bounds__(64) k_chan_graphs(const unsigned char* __restr
 struct PackJob {
   const float* S;
   u16* out;      // copy jobs: float* destination
+  // masked W copies (copy 2 with drop): the timestep's keep bits as well, in
+  // the layout of the pair dW product's GemmArgs::mbits (word
+  // (c * H + j) * W32 + i / 32, bit i % 32 = keep of W[c][i][j]); nullptr: none
+  uint32_t* bits;
   long sS, sO, lo_off, total;  // total: fragment-lanes (pack) or elements (copy)
   int ldS, K, N, trans, t, drop, copy;
 };
@@ -532,49 +536,62 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     if (J.trans) {
       // 16-byte pieces (the host sets trans when H % 4 == 0 and both ends are
       // 16-byte aligned): unmasked, J.total = C*H*H/4 float4s; masked, one
-      // thread per 4-row quad of 4 columns (J.total = C*(H/4)*(H/4)): the
-      // same Philox block per (c, row quad, column) as the scalar form
+      // thread per 32-row block of 4 columns (J.total = C*W32*(H/4)), walking
+      // its 8 row quads with the same Philox block per (c, row quad, column)
+      // as the scalar form, and storing the block's keep bits (4 words)
       if (!J.drop) {
         ((float4*)J.out)[q] = ((const float4*)J.S)[q];
         return;
       }
-      const int H = J.K, h4 = H >> 2;
-      const int j4 = (int)(q % h4), iq = (int)((q / h4) % h4), c = (int)(q / ((long)h4 * h4));
+      const int H = J.K, h4 = H >> 2, W32 = (H + 31) >> 5;
+      const int j4 = (int)(q % h4), w = (int)((q / h4) % W32), c = (int)(q / ((long)h4 * W32));
       if (a.chocc && !a.chocc[c]) return;  // a channel the staged batch does not use
-      const long e0 = ((long)c * H + 4 * iq) * H + 4 * j4;
-      float4 v[4];
+      uint32_t wb[4] = {0u, 0u, 0u, 0u};
+      for (int iq = 8 * w; iq < min(8 * w + 8, h4); ++iq) {
+        const long e0 = ((long)c * H + 4 * iq) * H + 4 * j4;
+        float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(J.S + e0 + (long)u * H);
+        for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(J.S + e0 + (long)u * H);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint4 w = edge_words(dr, c, 4 * iq, 4 * j4 + k, J.t);
+        for (int k = 0; k < 4; ++k) {
+          const uint4 x = edge_words(dr, c, 4 * iq, 4 * j4 + k, J.t);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float* x = (float*)&v[u] + k;
-          *x = drop_apply(dr, u4_get(w, u), *x);
+          for (int u = 0; u < 4; ++u) {
+            float* y = (float*)&v[u] + k;
+            *y = drop_apply(dr, u4_get(x, u), *y);
+            wb[k] |= (uint32_t)(u4_get(x, u) < dr.thr) << (4 * (iq - 8 * w) + u);
+          }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) *(float4*)((float*)J.out + e0 + (long)u * H) = v[u];
+        for (int u = 0; u < 4; ++u) *(float4*)((float*)J.out + e0 + (long)u * H) = v[u];
+      }
+      if (J.bits)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) J.bits[((long)c * H + 4 * j4 + k) * W32 + w] = wb[k];
       return;
     }
     if (!J.drop) {
       ((float*)J.out)[q] = J.S[q];
       return;
     }
-    // masked: one thread per 4-row quad of one column (J.total = C*HQ*H,
-    // HQ = ceil(H/4): the last quad of a W_c is partial when H % 4 != 0),
-    // whose 4 masks are the 4 words of one Philox block
-    const int H = J.K, hq = (H + 3) >> 2;
-    const int wj = (int)(q % H), iq = (int)((q / H) % hq), c = (int)(q / ((long)H * hq));
+    // masked: one thread per 32-row block of one column (J.total = C*W32*H),
+    // its row quads' 4 masks the 4 words of one Philox block each (the last
+    // quad of a W_c is partial when H % 4 != 0)
+    const int H = J.K, hq = (H + 3) >> 2, W32 = (H + 31) >> 5;
+    const int wj = (int)(q % H), w = (int)((q / H) % W32), c = (int)(q / ((long)H * W32));
     if (a.chocc && !a.chocc[c]) return;
-    const uint4 w = edge_words(dr, c, 4 * iq, wj, J.t);
+    uint32_t wb = 0u;
+    for (int iq = 8 * w; iq < min(8 * w + 8, hq); ++iq) {
+      const uint4 x = edge_words(dr, c, 4 * iq, wj, J.t);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (4 * iq + u >= H) break;
-      const long e = ((long)c * H + 4 * iq + u) * H + wj;
-      ((float*)J.out)[e] = drop_apply(dr, u4_get(w, u), J.S[e]);
+      for (int u = 0; u < 4; ++u) {
+        if (4 * iq + u >= H) break;
+        const long e = ((long)c * H + 4 * iq + u) * H + wj;
+        ((float*)J.out)[e] = drop_apply(dr, u4_get(x, u), J.S[e]);
+        wb |= (uint32_t)(u4_get(x, u) < dr.thr) << (4 * (iq - 8 * w) + u);
+      }
     }
+    if (J.bits) J.bits[((long)c * H + wj) * W32 + w] = wb;
     return;
   }
   const int per = (J.N / 32) * (J.K / 16) * 64;  // fragment-lanes per matrix

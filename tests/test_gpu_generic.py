@@ -440,6 +440,25 @@ def test_batch_pack_masks_only_the_batch_channels(mode):
         assert torch.equal(cf[u], cb[u]), t
         raw = pb.buf[o:o + n].view(C, h * h * 4)
         assert bool((raw[~u] == 0xFF).all()), t       # skipped copies: the sentinel, unwritten
+    # the keep bits the pack writes beside the copies (round 5: the pair dW
+    # product's mbits), after Wg, Wc and the occupancy bytes
+    w32 = (h + 31) // 32
+    ob = g_w + T * al(n) + al(4 * h * h * 4) + al(2 * h * h * 4) + al(C)
+    nbits = C * h * w32 * 4
+    u = torch.from_numpy(used).to(eng.device)
+    for t in range(T):
+        bf = pf.buf[ob + t * nbits:ob + (t + 1) * nbits].view(torch.int32).view(C, h * w32)
+        bb = pb.buf[ob + t * nbits:ob + (t + 1) * nbits].view(torch.int32).view(C, h * w32)
+        assert torch.equal(bf[u], bb[u]), t
+        assert bool((bb[~u] == -1).all()), t
+        # bit (i % 32) of word (c, j, i // 32): kept iff the masked copy is nonzero where W is
+        cf = pf.buf[g_w + t * al(n):g_w + t * al(n) + n].view(torch.float32).view(C, h, h).cpu().numpy()
+        words = bf.cpu().numpy().astype(np.uint32).reshape(C, h, w32)
+        i = np.arange(h)
+        keep = (words[:, :, i // 32] >> (i % 32)[None, None, :]) & 1      # [c][j][i]
+        wsrc = w["edge_weights"].reshape(C, h, h)
+        nz = wsrc != 0
+        assert np.array_equal((cf != 0)[nz], keep.transpose(0, 2, 1).astype(bool)[nz]), t
     eng.set_adjacency_edges(graphs[:2], v, E)
     with pytest.raises(RuntimeError):
         eng.forward(torch.zeros((2, v, h), device=eng.device), pb2, T)

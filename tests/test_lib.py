@@ -72,8 +72,9 @@ def test_dropout_dims_validation_and_sizes(lib):
     d2 = _lib.dims(256, 128, 256, 8, 5, edge_keep=0.9, state_keep=0.9, seed=3)
     d3 = _lib.dims(256, 128, 256, 8, 5, edge_keep=1.0, state_keep=0.9, seed=3)
     p1, p2 = _lib.weight_pack_bytes(d1), _lib.weight_pack_bytes(d2)
-    # (T-1) extra masked copies of W and W^T (hi + lo limbs) and of the general path's fp32 W
-    assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4)
+    # (T-1) extra masked copies of W and W^T (hi + lo limbs) and of the general path's fp32 W,
+    # and the general path's keep bits of every timestep (round 5: [T][C][h][h/32] words)
+    assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4) + 5 * 8 * 256 * 8 * 4
     assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
     # + the per-timestep dW scratch G [T][C][h][h], and the (T-1) C extra
     # per-timestep dW tiles' split-K partials (16 K chunks at b = 256, v = 128:
