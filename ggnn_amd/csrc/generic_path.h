@@ -23,7 +23,7 @@ struct GenAdjL {
   // pair mode (GGNN_SPARSE_PAIRS, k_pairs.h)
   size_t degc, pidx, pcnt, poff, prow, pdeg, ptile, pmask, wtl, wmap, wmask, wst;
   size_t rcnt, roff, rlist;  // reverse gather lists of the backward's dh scatter (k_pair_rev)
-  int cap_tiles, zw;  // product tiles of the pair-row capacity; dW split-K chunks
+  int cap_tiles, zw, chunk;  // product tiles of the pair-row capacity; dW split-K chunks and their tiles
 };
 GenAdjL gen_adj_layout(const Cfg& c) {
   GenAdjL L;
@@ -44,7 +44,8 @@ GenAdjL gen_adj_layout(const Cfg& c) {
   L.cgl = o; o += al((size_t)c.C * (c.b + 1) * 4);
   L.cgc = o; o += al((size_t)c.C * L.nch * (L.gch + 1) * 4);
   L.cap_tiles = (int)(c.pcap / PAIR_TILE);
-  L.zw = c.sparse ? L.cap_tiles / PAIR_CHUNK + c.C : 0;
+  L.chunk = pair_chunk(L.cap_tiles);
+  L.zw = c.sparse ? L.cap_tiles / L.chunk + c.C : 0;
   if (c.sparse) {
     const size_t N = (size_t)c.b * c.vin;
     L.degc = o;  o += al((size_t)c.C * N * 2);
@@ -55,7 +56,7 @@ GenAdjL gen_adj_layout(const Cfg& c) {
     L.pdeg = o;  o += al((size_t)c.pcap * 4);
     L.ptile = o; o += al((size_t)L.cap_tiles * 2 * 4);
     L.pmask = o; o += al((size_t)L.cap_tiles);
-    L.wtl = o;   o += al((size_t)L.zw * (1 + PAIR_CHUNK) * 4);
+    L.wtl = o;   o += al((size_t)L.zw * (1 + L.chunk) * 4);
     L.wmap = o;  o += al((size_t)L.zw * 4);
     L.wmask = o; o += al((size_t)L.zw);
     L.wst = o;   o += al((size_t)(c.C + 1) * 4);  // channel c's dW chunks: z in [wst[c], wst[c+1])
@@ -159,8 +160,9 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
     L.PZ = o;  o += al((size_t)c.pcap * H * 4);
     if (tr) {
       L.PDX = o; o += al((size_t)slices * L.pslice * 4);
-      const size_t zw = (c.pcap / PAIR_TILE) / PAIR_CHUNK + c.C;
-      L.WTL = o; o += al(zw * (1 + (size_t)c.T * PAIR_CHUNK) * 4);
+      const int cap_tiles = (int)(c.pcap / PAIR_TILE), ch = pair_chunk(cap_tiles);
+      const size_t zw = (size_t)(cap_tiles / ch) + c.C;
+      L.WTL = o; o += al(zw * (1 + (size_t)c.T * ch) * 4);
     }
   } else {
     L.M = o;   o += al((size_t)c.b * c.C * c.vin * H * 4);  // M (forward) / dM (backward), indexed by (g, c)
@@ -291,9 +293,20 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
       return GGNN_OK;
     }
     if (g_gemm_force >= 3) return fail(GGNN_EINVAL, "k_gemm_ks: fp32 k-contiguous A, one z, unscaled operands only");
+    // plain stores with no epilogue options (the weight-gradient split-K
+    // products, the pair products): the instance without the general
+    // epilogue, whose registers (256 VGPRs + 85 AGPRs at 128-row tiles) held
+    // one workgroup per CU
+    const bool lean = a.epi == GG_EPI_NONE && !a.dr.thr && !a.Nsplit &&
+                      (a.mode == GG_STORE || (a.mode == GG_ATOMIC && a.slab));
+    if (a.slab && !lean && !A16 && !small && a.tgroups <= 1)
+      return fail(GGNN_EINVAL, "k_gemm_ring: split-K slab partials with epilogue options (128-row tiles store slabs lean only)");
 #define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
-    if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
+    if (lean && !A16_ && BM_ == 128) {                                                                       \
+      if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, true, 2, 128, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
+      else hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, false, 2, 128, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
+    } else if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
     else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);    \
   } while (0)
 #define GGR(A16_, AKC_, BKC_)              \
@@ -376,7 +389,7 @@ int gen_set_adjacency_edges(const Cfg& c, void* adj, const int32_t* edges, const
     hipLaunchKernelGGL(k_pair_scan, dim3((unsigned)c.C), dim3(1024), 0, s, P<const u16>(adj, L.degc), N,
                        P<int>(adj, L.pidx), P<int>(adj, L.pcnt));
     hipLaunchKernelGGL(k_pair_layout, dim3(1), dim3(1024), 0, s, P<const int>(adj, L.pcnt), c.C, L.cap_tiles, L.zw,
-                       P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
+                       L.chunk, P<int>(adj, L.poff), P<int>(adj, L.ptile), P<unsigned char>(adj, L.pmask), P<int>(adj, L.wtl),
                        P<int>(adj, L.wmap), P<unsigned char>(adj, L.wmask), P<int>(adj, L.wst));
     hipLaunchKernelGGL(k_pair_fill, dim3(grid1d((long)c.C * N)), dim3(256), 0, s, P<const u16>(adj, L.degc),
                        P<int>(adj, L.pidx), P<const int>(adj, L.poff), N, (long)c.C * N, (int)c.pcap,
@@ -706,7 +719,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     }
   }
   if (c.sparse) {
-    // dW_c = sum_t mask_t (Y_t^T dXg_t), one launch: z = a chunk of <= PAIR_CHUNK
+    // dW_c = sum_t mask_t (Y_t^T dXg_t), one launch: z = a chunk of <= AL.chunk
     // tiles of one channel (zmap) with every timestep's copy of those tiles as
     // its terms (term q = t * cap_tiles + tile: the slices are cap_tiles tiles
     // apart); under edge dropout the accumulator is masked and banked at each
@@ -715,13 +728,13 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     {
       Prof p(K_WGRAD, s);
       hipLaunchKernelGGL(k_pair_wtl_expand, dim3((unsigned)((AL.zw + 255) / 256)), dim3(256), 0, s,
-                         P<const int>(adj, AL.wtl), AL.zw, c.T, AL.cap_tiles, P<int>(ws, L.WTL));
+                         P<const int>(adj, AL.wtl), AL.zw, c.T, AL.cap_tiles, AL.chunk, P<int>(ws, L.WTL));
     }
     GemmArgs a = gg_args();
     a.A = P<float>(ws, L.py(0)); a.sAm = 1; a.sAk = H; a.sAq = PAIR_TILE * H;
     a.B = P<float>(ws, L.pdx(0)); a.sBk = H; a.sBn = 1; a.sBq = PAIR_TILE * H;
     a.D = dW; a.sDp = H * H; a.sDm = H; a.sDn = 1; a.mode = GG_ATOMIC;
-    a.tl = P<const int>(ws, L.WTL); a.ts = 1 + (long)c.T * PAIR_CHUNK;
+    a.tl = P<const int>(ws, L.WTL); a.ts = 1 + (long)c.T * AL.chunk;
     a.zmap = P<const int>(adj, AL.wmap); a.zmask = P<const unsigned char>(adj, AL.wmask);
     a.Z = AL.zw; a.M = (int)H; a.N = (int)H; a.K = PAIR_TILE;
     // a channel's only chunk stores its dW (zmask 2); several chunks: slab
@@ -731,8 +744,12 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
 #ifdef GGNN_TS
     a.tsprobe = 1;
 #endif
+    // the term-group kernel also without dropout (banks unmasked): it holds
+    // two workgroups per CU where the plain ring holds one (round 5: b = 256
+    // reference step, dropout off, wgrad 0.96 -> 0.80 ms as the dropout-on run)
+    a.tgroups = c.T;
     if (c.ed) {
-      a.dr = c.edrop; a.tgroups = c.T;
+      a.dr = c.edrop;
       // the masks as bits: written by the pack beside its masked copies
       // (ggnn_pack_weights*, one Philox draw per weight and timestep for both)
       const int w32 = (int)((H + 31) / 32);

@@ -328,7 +328,10 @@ void slab_reduce_t(const GemmArgs& a, int G, const int* zs, int zsdiv, int nt, l
   memset(&r, 0, sizeof(r));
   r.slab = a.slab; r.sSlab = a.sSlab; r.zT = zT; r.D = a.D; r.sDg = (long)a.M * a.N; r.sDm = a.sDm;
   r.M = a.M; r.N = a.N; r.G = G; r.zs = zs; r.zsdiv = zsdiv; r.nt = nt; r.ugmax = ugmax;
-  slab_launch(r, s);
+  const long n = (long)r.M * r.N;
+  const bool v4 = r.N % 4 == 0 && r.sSlab % 4 == 0 && (r.zT * r.sSlab) % 4 == 0 && ((uintptr_t)r.slab & 15) == 0;
+  if (v4) hipLaunchKernelGGL(k_seg_reduce<4>, dim3((unsigned)((n / 4 + 3) / 4), (unsigned)G), dim3(256), 0, s, r);
+  else hipLaunchKernelGGL(k_seg_reduce<1>, dim3((unsigned)((n + 3) / 4), (unsigned)G), dim3(256), 0, s, r);
 }
 
 WsL ws_layout(const Cfg& c, bool training) {

@@ -87,8 +87,12 @@ DEV void ring_tile(int nwg, int tm, int tn, int& z, int& mt, int& nt) {
 // waves per EU (two workgroups per CU: 238 VGPRs, no AGPRs; at 1 it held 249 +
 // 64 AGPRs, one workgroup per CU, 1.37 vs 0.95 ms) and banks from ONE call site
 // (the unrolled slot loop inlined it twice).
-template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT, bool TGRP = false>
-__global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int tm, int tn) {
+// LEAN: the host guarantees plain stores (GG_STORE, or GG_ATOMIC into a slab /
+// a sole chunk) with no activation, dropout or column split (an E factor and a
+// bias are taken): only the lean epilogue is compiled, and the kernel asks for
+// 2 waves per EU
+template <int PREC, bool A16, bool AKC, bool BKC, bool SCALE, int NBUF, int BMT, bool TGRP = false, bool LEAN = false>
+__global__ void __launch_bounds__(256, TGRP || LEAN ? 2 : 1) k_gemm_ring(GemmArgs a, int tm, int tn) {
   const Drop dr = drop_resolve(a.dr);  // (a device-resident key: loaded once)
   using namespace gr;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
@@ -320,12 +324,9 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
 #pragma unroll
   for (int u = 0; u < NBUF - 1; ++u)
     if (u < nit) stage(u, slot(u));
-  if constexpr (NBUF == 2) {
-    // one call site of compute (and of the masked banking, which inlined twice
-    // in the unrolled slot loop): the slot is picked at run time.  (The
-    // 128-row tiles without term groups hold 256 VGPRs + 85 AGPRs either way,
-    // one workgroup per CU; forcing two per CU spills 88 B per lane and
-    // measured no faster at the 20-sentence batch or at config 3, round 5)
+  if constexpr (TGRP && NBUF == 2) {
+    // one call site of the masked banking (the unrolled slot loop inlined it
+    // twice): the slot is picked at run time
     for (int it = 0; it < nit; ++it) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMAs of slice it landed; slice it-1 fully read
@@ -376,9 +377,13 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
   // scalar stores of a 128 x 128 tile took ~8 us, one outstanding-store
   // window after another.  Same arithmetic, same bits.
   const bool to_slab = a.mode == GG_ATOMIC && !sole;
-  const bool lean = !a.E && a.epi == GG_EPI_NONE && (TGRP || !dr.thr) && !a.Nsplit &&
-                    (a.mode == GG_STORE || sole || (to_slab && a.slab));
-  if (lean) {
+  // (LEAN instances, chosen by the host, and the term-group products; the
+  // other instances keep only the general epilogue: the lean one's registers
+  // on top cost them their second workgroup per CU -- 256 VGPRs + 85 AGPRs
+  // against round 4's 188 + 64, +30-50 % at b = 256, round 5)
+  const bool lean = LEAN || (TGRP && !a.E && a.epi == GG_EPI_NONE && !a.Nsplit &&
+                             (a.mode == GG_STORE || sole || (to_slab && a.slab)));
+  if constexpr (LEAN || TGRP) if (lean) {
     float* const Db = to_slab ? a.slab + (long)z * a.sSlab : a.D + dbase;
     const long sm = to_slab ? (long)a.N : a.sDm, sn = to_slab ? 1 : a.sDn;
     constexpr int WR = AM * 32, WC = AN * 32, C4 = WC / 4;  // a wave's tile, its 16-byte chunks per row
@@ -396,12 +401,26 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
       if (n < a.N) {
         const float bn = bias ? bias[n] : 0.f;
         float* const Dc = Db + (long)n * sn;
+        // E factors (the heads' dropout-scaled weight gradient) at D's
+        // coordinates, loaded up front (the stores below may alias them)
+        float ef[LEAN ? AM : 1][16];
+        if constexpr (LEAN)
+          if (a.E) {
+            const float* Ec = a.E + dbase + (long)n * a.sDn;
+#pragma unroll
+            for (int i = 0; i < AM; ++i)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                ef[i][r] = Ec[(long)min(m0 + wm * AM * 32 + 32 * i + acc_row(r, hh), a.M - 1) * a.sDm];
+          }
 #pragma unroll
         for (int i = 0; i < AM; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = 32 * i + acc_row(r, hh), m = m0 + wm * AM * 32 + rl;
-            const float x = gs.alpha * (TGRP ? bank[i][j][r] : acc[i][j][r]) + bn;
+            float x = gs.alpha * (TGRP ? bank[i][j][r] : acc[i][j][r]) + bn;
+            if constexpr (LEAN)
+              if (a.E) x *= ef[i][r];
             if (m < a.M) cs += x;
             if (vec) park[pk_off(rl, 32 * j + l32)] = x;
             else if (m < a.M) Dc[(long)m * sm] = x;
@@ -429,6 +448,7 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
     if (tsk >= 0) TSMARK(tsk, 3);
     return;
   }
+  if constexpr (LEAN) return;  // (the lean epilogue above took every case)
   if (!live) return;  // nothing of this wave's to store (no barrier follows)
 
   // ---- epilogue (as k_gemm)
@@ -476,8 +496,16 @@ __global__ void __launch_bounds__(256, TGRP ? 2 : 1) k_gemm_ring(GemmArgs a, int
           cs += x;
           float* d = Dn + doff;
           if (a.mode == GG_ATOMIC && !sole) {
-            if (a.slab) a.slab[(long)z * a.sSlab + (long)m * a.N + n] = x;
-            else atomicAdd(d, x);
+            // (128-row tiles of fp32 operands: slab products always take the
+            // lean epilogue -- gg_launch sends them to the LEAN instances --
+            // and this one keeps round 4's registers: 188 VGPRs + 64 AGPRs,
+            // two workgroups per CU)
+            if (A16 || BMT != 128) {
+              if (a.slab) a.slab[(long)z * a.sSlab + (long)m * a.N + n] = x;
+              else atomicAdd(d, x);
+            } else {
+              atomicAdd(d, x);
+            }
           }
           else if (a.mode == GG_ADD) *d = (EPI_PRE ? pre[EPI_PRE ? i : 0][r] : *d) + x;
           else *d = x;

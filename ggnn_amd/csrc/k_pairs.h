@@ -21,18 +21,20 @@
 // the results are deterministic.  Backward (same
 // decomposition): dXg_p = dX[row_p]; dY = dXg W_c^T; dh[g,j] += sum over pairs
 // with A[g,c,i,j] = 1 of dY_p; dW_c += Y_c^T dXg_c (split-K over chunks of
-// PAIR_CHUNK tiles, the edge-dropout mask applied in the product's epilogue);
+// pair_chunk() tiles, the edge-dropout mask applied in the product's epilogue);
 // dbeta_c += sum_p deg_p dXg_p.
 #pragma once
 #include "ggnn_common.h"
 
 #define PAIR_TILE 32   // rows per product tile (the ring kernel's 32-row variant)
-// tiles per split-K term list of the dW product (128 rows).  16 (512 rows) was
-// the atomic-era choice (4 and 8 meant more chunks, more atomics); with slab
-// partials a shorter list caps the longest workgroup's walk instead (a
-// 20-sentence batch's busiest channel: 64 -> 16 slices; with the ring's lean
-// epilogue the product went 159 -> 105 us, tools/ts_probe_generic.py, round 5)
-#define PAIR_CHUNK 4
+// tiles per split-K term list of the dW product: 4 (128 rows) at small
+// batches, 16 (512 rows) at large ones (pair_chunk).  16 was the atomic-era
+// choice everywhere; with slab partials a shorter list caps the longest
+// workgroup's walk at the 20-sentence batch (its busiest channel: 64 -> 16
+// slices; with the ring's lean epilogue the product went 159 -> 105 us,
+// tools/ts_probe_generic.py), while at b = 256 the 4x more slab partials cost
+// more than the walk saves (wgrad 0.958 vs 1.038 ms per step, round 5)
+HDI int pair_chunk(int cap_tiles) { return cap_tiles <= 512 ? 4 : 16; }
 
 // S1: in-degree per (channel, node row) from the staged 16-bit rows (0/1
 // limbs: nonzero bits <=> 1); one block per (graph, channel) tile, a wave per row
@@ -88,11 +90,12 @@ __global__ void __launch_bounds__(1024) k_pair_scan(const u16* __restrict__ degc
 
 // S3: channel offsets (padded to PAIR_TILE), the per-tile term lists of the
 // products (ptile[2z] = 1 live / 0 dead, ptile[2z+1] = channel; pmask), and the
-// dW product's split-K chunks (wtl[z*(1+PAIR_CHUNK)] = tile count, then the
+// dW product's split-K chunks (wtl[z*(1+chunk)] = tile count, then the
 // tile indices; wmap[z] = channel; wmask: 1 live, 2 live and its channel's
 // only chunk, whose dW tiles are then stored instead of added atomically:
 // fp32 atomics bound the dW product at small batches, ~65 G adds/s).  One block.
 __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pcnt, int C, int cap_tiles, int zw_cap,
+                                                      int chunk,
                                                       int* __restrict__ poff, int* __restrict__ ptile,
                                                       unsigned char* __restrict__ pmask, int* __restrict__ wtl,
                                                       int* __restrict__ wmap, unsigned char* __restrict__ wmask,
@@ -106,7 +109,7 @@ __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pc
       cst[c] = ch;
       const int t = (pcnt[c] + PAIR_TILE - 1) / PAIR_TILE;
       off += t * PAIR_TILE;
-      ch += (t + PAIR_CHUNK - 1) / PAIR_CHUNK;
+      ch += (t + chunk - 1) / chunk;
     }
     soff[C] = off;
     cst[C] = ch;
@@ -134,13 +137,13 @@ __global__ void __launch_bounds__(1024) k_pair_layout(const int* __restrict__ pc
     pmask[z] = live ? 1 : 0;
   }
   for (int z = tid; z < zw_cap; z += blockDim.x) {
-    int* q = wtl + (long)z * (1 + PAIR_CHUNK);
+    int* q = wtl + (long)z * (1 + chunk);
     if (z < cst[C]) {
       const int c = find(cst, z), j = z - cst[c];
       const int t0 = soff[c] / PAIR_TILE, nt = (soff[c + 1] - soff[c]) / PAIR_TILE;
-      const int cnt = min(PAIR_CHUNK, nt - j * PAIR_CHUNK);
+      const int cnt = min(chunk, nt - j * chunk);
       q[0] = cnt;
-      for (int e = 0; e < cnt; ++e) q[1 + e] = t0 + j * PAIR_CHUNK + e;
+      for (int e = 0; e < cnt; ++e) q[1 + e] = t0 + j * chunk + e;
       wmap[z] = c;
       wmask[z] = cst[c + 1] - cst[c] == 1 ? 2 : 1;  // 2: the channel's only chunk (k_gemm_ring stores)
     } else {
@@ -171,13 +174,14 @@ __global__ void k_pair_fill(const u16* __restrict__ degc, int* __restrict__ pidx
 
 
 // B5: the dW product's term lists over all T timesteps: chunk z's tiles
-// (wtl[z*(1+PAIR_CHUNK)]) repeated per timestep as q = t * cap_tiles + tile,
+// (wtl[z*(1+chunk)]) repeated per timestep as q = t * cap_tiles + tile,
 // t ascending (groups of equal size: GemmArgs::tgroups)
-__global__ void k_pair_wtl_expand(const int* __restrict__ wtl, int zw, int T, int cap_tiles, int* __restrict__ out) {
+__global__ void k_pair_wtl_expand(const int* __restrict__ wtl, int zw, int T, int cap_tiles, int chunk,
+                                  int* __restrict__ out) {
   const int z = blockIdx.x * blockDim.x + threadIdx.x;
   if (z >= zw) return;
-  const int* q = wtl + (long)z * (1 + PAIR_CHUNK);
-  int* o = out + (long)z * (1 + (long)T * PAIR_CHUNK);
+  const int* q = wtl + (long)z * (1 + chunk);
+  int* o = out + (long)z * (1 + (long)T * chunk);
   const int n = q[0];
   o[0] = n * T;
   for (int t = 0; t < T; ++t)
