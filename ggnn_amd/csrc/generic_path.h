@@ -303,9 +303,9 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
       return fail(GGNN_EINVAL, "k_gemm_ring: split-K slab partials with epilogue options (128-row tiles store slabs lean only)");
 #define GGR1(A16_, AKC_, BKC_, BM_)                                                                          \
   do {                                                                                                       \
-    if (lean && !A16_ && BM_ == 128) {                                                                       \
-      if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, true, 2, 128, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
-      else hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, false, 2, 128, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
+    if (lean && !A16_) {                                                                                     \
+      if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, true, 2, BM_, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
+      else hipLaunchKernelGGL((k_gemm_ring<PREC, false, AKC_, BKC_, false, 2, BM_, false, true>), grid, dim3(256), 0, s, a, tm, tn); \
     } else if (sc) hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, true, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);  \
     else hipLaunchKernelGGL((k_gemm_ring<PREC, A16_, AKC_, BKC_, false, 2, BM_>), grid, dim3(256), 0, s, a, tm, tn);    \
   } while (0)
@@ -470,7 +470,9 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     if (c.sparse) {
       // pair mode (k_pairs.h): Y = A h, Z = Y W_c per 32-row tile, X = the
       // row's sum of Z + deg beta
-      float* PY = P<float>(ws, L.PY);
+      // (training: Y_t into timestep t's slice, kept for the backward's dW
+      // product instead of regathered there)
+      float* PY = P<float>(ws, tr ? L.py(t) : L.PY);
       float* PZ = P<float>(ws, L.PZ);
       {
         Prof p(K_PROP_FWD, s);
@@ -618,14 +620,13 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
     }
     if (c.sparse) {
-      // pair mode (k_pairs.h): Y_t recomputed from the saved h_t, dXg = dX
-      // of the pair rows, dbeta, dY = dXg W_c^T, dh += A^T dY, dW_c += Y^T dXg
-      float* PY = P<float>(ws, L.py(t));
+      // pair mode (k_pairs.h): Y_t as the training forward left it in its
+      // slice, dXg = dX of the pair rows, dbeta, dY = dXg W_c^T, dh += A^T dY,
+      // dW_c += Y^T dXg
       float* PZ = P<float>(ws, L.PZ);
       float* PDX = P<float>(ws, L.pdx(t));
       {
         Prof p(K_PROP_BWD, s);
-        gen_pairs_y(c, AL, adj, ht, PY, s);
         // dXg gathered, with the dbeta partial of every pair tile (one
         // channel's rows): sum of deg * dXg, summed per channel in tile order
         // after the timestep loop
