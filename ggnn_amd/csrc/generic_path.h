@@ -320,6 +320,8 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else if (AKC && BKC) GGR(false, true, true);
     else if (!AKC && !BKC && a.tgroups > 1) {
       if (a.dr.thr && !a.mbits) return fail(GGNN_EINVAL, "k_gemm_ring: masked term groups need the mask bits (the pack's)");
+      // (whole z's round-robin over the XCDs: the grid covers a multiple of 8 z's)
+      const dim3 grid((unsigned)((long)tn * tm * ((a.Z + 7) / 8) * 8));
       // (a 4-slot ring, three slices in flight at one workgroup per CU, measured
       // slower for the weight-gradient products: 1.37 -> 1.72 ms at the
       // reference configuration)

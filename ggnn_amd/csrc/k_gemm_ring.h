@@ -119,7 +119,21 @@ __global__ void __launch_bounds__(256, TGRP || LEAN ? 2 : 1) k_gemm_ring(GemmArg
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int wm = w % WMW, wn = w / WMW;
   int z, mt, ntile;
-  ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  if constexpr (TGRP) {
+    // term groups (the pair dW: z = a chunk of one channel's tiles, chunks of
+    // very different lengths in channel order): whole z's round-robin over
+    // the 8 XCDs (z % 8 = the XCD), a z's output tiles together on its XCD
+    // (they share its operand rows).  ring_tile's contiguous runs of z per
+    // XCD piled the heavy channels' chunks onto one or two XCDs.  The host
+    // rounds the grid up to a multiple of 8 z's.
+    const int bid = blockIdx.x, per = tm * tn, q8 = bid >> 3;
+    z = (bid & 7) + 8 * (q8 / per);
+    const int t = q8 - (q8 / per) * per;
+    mt = t / tn;
+    ntile = t - mt * tn;
+  } else {
+    ring_tile(gridDim.x, tm, tn, z, mt, ntile);
+  }
   const int tsk = a.tsprobe - 1;
   if (tsk >= 0) TSMARK(tsk, 0);
   if (z >= a.Z) return;
