@@ -250,8 +250,11 @@ DEV void gb_mma(f32x16& a1, f32x16& a2, frag ah, frag al, const W& w) {
   }
 }
 
+#ifndef GGNN_GB_RT1_OCC
+#define GGNN_GB_RT1_OCC 1
+#endif
 template <int H, int RT, int PREC>
-__global__ void __launch_bounds__(2 * H)
+__global__ void __launch_bounds__(2 * H, RT == 1 ? 2 * GGNN_GB_RT1_OCC : 1)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
@@ -262,6 +265,9 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   // (summed in a fixed order by k_sum_rows: deterministic), or nullptr: atomics
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16, WH = SPLIT && GGNN_GB_WHI;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
+  // two 32-row workgroups per CU (GGNN_GB_RT1_OCC = 2) fit the 128-VGPR budget
+  // with a one-deep weight ring; the other workgroup hides its latency
+  constexpr int GBD = RT == 1 && GGNN_GB_RT1_OCC == 2 ? 1 : GB_DEPTH;
   const float ds = gscale(gmax);  // gradient scale of dL/dh_T read in place (ggnn_common.h), else 1
   typedef Swz<ZCH> SZ;
   constexpr int NIMG = SPLIT ? 2 : 1;
@@ -335,7 +341,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
                 frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
   };
-  b_pipeline<KS, GB_DEPTH, GB_UNROLL>(ld1, [&](int ks, const auto& w) {
+  b_pipeline<KS, GBD, GB_UNROLL>(ld1, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
@@ -387,7 +393,7 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
                 frag_ld(WgTp, NS + ns, ks, 2 * KS, lane),
                 SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
   };
-  b_pipeline<2 * KS, GB_DEPTH, GB_UNROLL>(ld2, [&](int ks, const auto& w) {
+  b_pipeline<2 * KS, GBD, GB_UNROLL>(ld2, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
