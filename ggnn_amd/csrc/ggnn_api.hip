@@ -535,6 +535,10 @@ struct launch_gru_bwd_tag {};
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
 template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
+#ifndef GGNN_GB_MAXRT
+#define GGNN_GB_MAXRT 2
+#endif
+template <> struct kSplitRT<launch_gru_bwd_tag> { static constexpr int value = GGNN_GB_MAXRT; };
 
 void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,
                  int batch, hipStream_t s, Drop dr = Drop{0, 0, 0, 1.0f}, int t = 0) {
