@@ -238,11 +238,27 @@ static thread_local int g_gemm_force = 0;
 
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
+// the fused r * h output of a gates product (GemmArgs::aux) as its own pass,
+// behind the instances whose epilogue does not carry it
+inline void gen_rh_after(const GemmArgs& a, hipStream_t s) {
+  if (a.aux)
+    hipLaunchKernelGGL(k_gen_rh, dim3(grid1d((long)a.M * a.auxN)), dim3(256), 0, s, (const float*)a.D, a.auxin,
+                       a.aux, (long)a.M, a.auxN);
+  if (a.bout)
+    hipLaunchKernelGGL(k_gen_blend, dim3(grid1d((long)(a.M / a.bv) * ((a.bv + 3) / 4) * a.N)), dim3(256), 0, s,
+                       a.bu, a.bh, (const float*)a.D, a.bout, (long)a.M, a.N, a.bv, a.bsd, a.bt);
+}
 template <int PREC>
 int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s) {
   if (a.Z < 1 || a.M < 1 || a.N < 1) return GGNN_OK;
   if (a.Ktot == 0) a.Ktot = a.K;
   if (a.E && a.mode == GG_ADD) return fail(GGNN_EINVAL, "gemm: an E factor with GG_ADD (the epilogue preloads one of them)");
+  if (a.aux && (a.E || a.mode != GG_STORE || a.epi != GG_EPI_SIGMOID || a.Z != 1 || a.Nsplit || a.dr.thr ||
+                a.sDm != 2L * a.auxN || a.sDn != 1 || a.N != 2 * a.auxN))
+    return fail(GGNN_EINVAL, "gemm: the fused r * h output takes the plain [M][2 auxN] gates store only");
+  if (a.bout && (a.E || a.mode != GG_STORE || a.epi != GG_EPI_TANH || a.Z != 1 || a.Nsplit || a.dr.thr ||
+                 a.sDm != a.N || a.sDn != 1 || a.bv < 1 || a.M % a.bv))
+    return fail(GGNN_EINVAL, "gemm: the fused blend takes the plain [M][N] candidate store only");
   if (g_gemm_force != 1 && ring_ok(a, A16, AKC, BKC)) {
     // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
     // per-(graph, channel) products of v = 30 sentence graphs), and for
@@ -292,6 +308,10 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
 #undef GKS
       return GGNN_OK;
     }
+    // the ring instances keep their epilogue: r * h by its own pass after them
+    const GemmArgs rh = a;
+    a.aux = nullptr;
+    a.bout = nullptr;
     if (g_gemm_force >= 3) return fail(GGNN_EINVAL, "k_gemm_ks: fp32 k-contiguous A, one z, unscaled operands only");
     // plain stores with no epilogue options (the weight-gradient split-K
     // products, the pair products): the instance without the general
@@ -331,6 +351,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     else return fail(GGNN_EINVAL, "k_gemm_ring: operand layout combination not compiled");
 #undef GGR
 #undef GGR1
+    gen_rh_after(rh, s);
     return GGNN_OK;
   }
   if (a.tgroups > 1) return fail(GGNN_EUNSUP, "per-timestep term groups need the ring kernel (16-byte aligned operands)");
@@ -349,6 +370,7 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   else if (!A16 && !AKC && !BKC) GGL(false, false, false);
   else return fail(GGNN_EINVAL, "k_gemm: operand layout combination not compiled");
 #undef GGL
+  gen_rh_after(a, s);
   return GGNN_OK;
 }
 
@@ -516,12 +538,8 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     gt.bias = P<float>(pack, PL.bg);
     gt.nterm = 2;
     gt.M = (int)N; gt.N = (int)(2 * H); gt.K = (int)H; gt.epi = GG_EPI_SIGMOID;
+    gt.aux = P<float>(ws, L.rh(t)); gt.auxin = P<const float>(ws, hin); gt.auxN = (int)H;  // + r h
     if (int e = gg_launch<PREC>(gt, false, true, false, K_GRU_FWD, s)) return e;
-    {
-      Prof p(K_GRU_FWD, s);
-      hipLaunchKernelGGL(k_gen_rh, dim3(grid1d(N * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
-                         P<const float>(ws, hin), P<float>(ws, L.rh(t)), N, c.H);
-    }
     // cc = tanh([X, r h] Wc + bc)
     GemmArgs cd = gg_args();
     cd.A = P<float>(ws, L.x(t)); cd.sAq = ((long)L.rh(t) - (long)L.x(t)) / 4; cd.sAm = H; cd.sAk = 1;
@@ -530,12 +548,10 @@ int gen_forward(const Cfg& c, const void* pack, void* adj, void* ws, bool tr, co
     cd.bias = P<float>(pack, PL.bc);
     cd.nterm = 2;
     cd.M = (int)N; cd.N = (int)H; cd.K = (int)H; cd.epi = GG_EPI_TANH;
+    // + h' = u h + (1 - u) c and the state dropout
+    cd.bout = hout; cd.bh = P<const float>(ws, hin); cd.bu = P<const float>(ws, L.g(t));
+    cd.bv = (int)c.vin; cd.bt = t; cd.bsd = c.sdrop;
     if (int e = gg_launch<PREC>(cd, false, true, false, K_GRU_FWD, s)) return e;
-    {
-      Prof p(K_GRU_FWD, s);
-      hipLaunchKernelGGL(k_gen_blend, dim3(grid1d((long)c.b * ((c.vin + 3) / 4) * H)), dim3(256), 0, s, P<const float>(ws, L.g(t)),
-                         P<const float>(ws, hin), P<const float>(ws, L.cc(t)), hout, N, c.H, c.vin, c.sdrop, t);
-    }
   }
   LAUNCHCHK();
   return GGNN_OK;

@@ -350,6 +350,9 @@ DEV uint4 edge_words(const Drop& d, int c, int i, int j, int t) {
   return philox4x32_10(make_uint4((uint32_t)i >> 2, (uint32_t)j, (uint32_t)c, (uint32_t)t), dkey0(d), dkey1(d));
 }
 DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x * d.scale : 0.0f; }
+// the GRU state update h' = u h + (1 - u) c with one rounding order wherever
+// it is formed (k_gen_blend, k_gemm_ks's fused epilogue)
+DEV float gru_blend(float u, float h, float c) { return __builtin_fmaf(u, h, (1.0f - u) * c); }
 
 // ---- backward gradient scaling.  The btb loss is divided by the number of
 // targets (chem_tensorflow.py:360,399-403), so dL/dh_T arrives at ~1/b per

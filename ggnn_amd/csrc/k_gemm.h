@@ -110,6 +110,22 @@ struct GemmArgs {
   // (gunscale, ggnn_common.h), so a weight-gradient product stores final
   // values (S a power of two: the same bits as unscaling afterwards)
   const uint32_t* ugmax;
+  // if set (GG_EPI_SIGMOID, the GRU gates [r | u] of width 2 auxN): the
+  // reset-gated state aux[m * auxN + n] = r * auxin[m * auxN + n] for the
+  // columns n < auxN, stored next to the gates (k_gemm_ks's epilogue; after
+  // a ring launch gg_launch runs k_gen_rh instead)
+  float* aux;
+  const float* auxin;
+  int auxN;
+  // if set (GG_EPI_TANH, the GRU candidate c of width N): the blended state
+  // bout[m * N + n] = u h + (1 - u) c, u = bu[m * 2N + N + n], h = bh[m * N + n],
+  // then the state dropout bsd of timestep bt (graphs of bv rows), as
+  // k_gen_blend computes it (k_gemm_ks's epilogue; else k_gen_blend after)
+  float* bout;
+  const float* bh;
+  const float* bu;
+  int bv, bt;
+  Drop bsd;
   // -DGGNN_TS experiment builds: k + 1 = record this launch's per-workgroup
   // phase stamps in g_ts[k] (tools/ts_probe_generic.py); 0 = none
   int tsprobe;

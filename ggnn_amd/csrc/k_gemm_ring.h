@@ -701,13 +701,29 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
   float* const Dn = hi_n ? a.D2 : a.D;
   const long sm = hi_n && a.sD2m ? a.sD2m : a.sDm, dn = dbase + (long)(hi_n ? n - a.Nsplit : n) * a.sDn;
   // E factors / old D values (GG_ADD) loaded up front (as k_gemm_ring)
-  float pre[16 / WK];
+  // (or the state h of the fused r * h output, GemmArgs::aux)
+  float pre[16 / WK], pre2[16 / WK];
+  const bool rhn = a.aux && n < a.auxN, bln = a.bout != nullptr;
   if (a.E || a.mode == GG_ADD) {
     const float* src = a.E ? a.E : Dn;
 #pragma unroll
     for (int e = 0; e < 16 / WK; ++e)
       pre[e] = src[dn + (long)min(m0 + acc_row(4 * (wk * (4 / WK) + (e >> 2)), hh) + (e & 3), a.M - 1) * sm];
+  } else if (rhn) {
+#pragma unroll
+    for (int e = 0; e < 16 / WK; ++e)
+      pre[e] = a.auxin[(long)min(m0 + acc_row(4 * (wk * (4 / WK) + (e >> 2)), hh) + (e & 3), a.M - 1) * a.auxN + n];
+  } else if (bln) {
+#pragma unroll
+    for (int e = 0; e < 16 / WK; ++e) {
+      const long row = min(m0 + acc_row(4 * (wk * (4 / WK) + (e >> 2)), hh) + (e & 3), a.M - 1);
+      pre[e] = a.bh[row * a.N + n];
+      pre2[e] = a.bu[row * 2 * a.N + a.N + n];
+    }
   }
+  const Drop sd = bln ? drop_resolve(a.bsd) : Drop{};
+  long wkey = -1;  // the first row of the state-dropout quad whose words w holds
+  uint4 sw = make_uint4(0u, 0u, 0u, 0u);
   float cs = 0.f;
 #pragma unroll
   for (int qq = 0; qq < 4 / WK; ++qq) {
@@ -731,6 +747,20 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
       float x = gs.alpha * v + bn;
       if (a.epi == GG_EPI_SIGMOID) x = sigm(x);
       else if (a.epi == GG_EPI_TANH) x = tanh_f(x);
+      if (rhn) a.aux[(long)m * a.auxN + n] = x * pre[4 * qq + r4];
+      if (bln) {
+        const float ug = pre2[4 * qq + r4];
+        float y = gru_blend(ug, pre[4 * qq + r4], x);
+        if (sd.thr) {
+          const int g = m / a.bv, i = m - g * a.bv;
+          if ((long)m - (i & 3) != wkey) {
+            wkey = (long)m - (i & 3);
+            sw = state_words(sd, g, i, n, a.bt);
+          }
+          y = drop_apply(sd, u4_get(sw, i & 3), y);
+        }
+        a.bout[(long)m * a.N + n] = y;
+      }
       if (dr.thr) x = drop_apply(dr, u4_get(dq, r4), x);
       const long doff = dn + (long)m * sm;
       if (a.E) x *= pre[4 * qq + r4];

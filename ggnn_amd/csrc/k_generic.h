@@ -165,7 +165,7 @@ __global__ void k_gen_blend(const float* __restrict__ G, const float* __restrict
       if (u >= x.nr) break;
       const long row = x.row0 + u, e = row * H + x.k;
       const float ug = G[row * 2 * H + H + x.k];
-      float y = ug * h[e] + (1.0f - ug) * cc[e];
+      float y = gru_blend(ug, h[e], cc[e]);
       if (sd.thr) y = drop_apply(sd, u4_get(w, u), y);
       hout[e] = y;
     }
