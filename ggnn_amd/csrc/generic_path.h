@@ -79,7 +79,8 @@ struct GenWsL {
   // products (GemmArgs::slab), the element-wise kernels' bias partials
   // [T][slices][dbg_r | dbg_u | dbc], pair mode's per-tile dbeta partials
   // [T][cap_tiles][H], and k_sum_rows' chunk sums
-  size_t SLAB, GBP, PDB, SUMS, CSP;  // CSP: the dense tiles' dbeta column-sum partials [b][C][v/32][H]
+  size_t SLAB, GBP, GBR, PDB, SUMS, CSP;  // GBR: dbg_r partials of the fused k_gen_bwd2 [T][M/32 * 4][H]
+   // CSP: the dense tiles' dbeta column-sum partials [b][C][v/32][H]
   size_t py(int t) const { return PY + (size_t)t * pslice * 4; }
   size_t pdx(int t) const { return PDX + (size_t)t * pslice * 4; }
   size_t nh, ns;  // floats of one [N][H] array; saved-step slots
@@ -177,6 +178,7 @@ GenWsL gen_ws_layout(const Cfg& c, bool tr) {
     L.gmax = o; o += al(GMAX_BYTES);
     L.SLAB = o; o += al(gen_slab_floats(c) * 4);
     L.GBP = o;  o += al((size_t)c.T * gen_bias_slices(c) * 3 * H * 4);
+    L.GBR = o;  o += al((size_t)c.T * ((N + 31) / 32) * 4 * H * 4);
     if (c.sparse) { L.PDB = o; o += al((size_t)c.T * (c.pcap / PAIR_TILE) * H * 4); }
     L.SUMS = o; o += al((size_t)SUM_RCS * (3 * H + c.C * H) * 4);
     if (!c.sparse) { L.CSP = o; o += al((size_t)c.b * c.C * ((c.vin + 31) / 32) * H * 4); }
@@ -238,6 +240,28 @@ static thread_local int g_gemm_force = 0;
 
 // operand layouts: AKC = A[m][k] with k contiguous, else m contiguous;
 // BKC = B stored [n][k] (k contiguous), else B[k][n] (n contiguous)
+// k_gemm_ks's column split for a product (0: not a k_gemm_ks product): K
+// split over the waves for one-z products whose 32-row grid leaves the chip
+// mostly idle and walks >= 8 K slices (the GRU products of a 20-sentence
+// batch): the narrowest column split whose grid stays within two workgroups
+// per CU.  (Not for term-listed tiles: over the pair tiles of a 20-sentence
+// batch 32 x 32 tiles measured slower -- prop_fwd 0.226 -> 0.249 ms per step,
+// W_c and Y re-read per column block -- and a graph's channel list would hand
+// the waves other terms under channel skipping, which must stay bit-identical
+// to the dense loop.)
+int gg_ks_wn(GemmArgs a, bool A16, bool AKC, bool BKC) {
+  if (a.Ktot == 0) a.Ktot = a.K;
+  if (g_gemm_force == 1 || !ring_ok(a, A16, AKC, BKC)) return 0;
+  const long grid128 = (long)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.Z;
+  const bool small = AKC && (a.M <= 64 || grid128 < 128);
+  const bool sc = a.scA != 1.0f || a.scB != 1.0f || a.snum;
+  const long kslices = (long)((a.K + 31) / 32) * std::max(a.nterm, 1);
+  if (A16 || !AKC || sc || a.tgroups > 1 || a.Z != 1 || a.tl) return 0;
+  if (g_gemm_force >= 3) return 1 << (g_gemm_force - 3);  // forced: 3 -> WN 1, 4 -> 2, 5 -> 4
+  for (int c = 1; c <= 4 && small && kslices >= 8 && g_gemm_force != 2; c *= 2)
+    if ((long)((a.M + 31) / 32) * ((a.N + 32 * c - 1) / (32 * c)) <= 512) return c;
+  return 0;
+}
 // the fused r * h output of a gates product (GemmArgs::aux) as its own pass,
 // behind the instances whose epilogue does not carry it
 inline void gen_rh_after(const GemmArgs& a, hipStream_t s) {
@@ -259,6 +283,9 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
   if (a.bout && (a.E || a.mode != GG_STORE || a.epi != GG_EPI_TANH || a.Z != 1 || a.Nsplit || a.dr.thr ||
                  a.sDm != a.N || a.sDn != 1 || a.bv < 1 || a.M % a.bv))
     return fail(GGNN_EINVAL, "gemm: the fused blend takes the plain [M][N] candidate store only");
+  if (a.b2dzg && (a.E || a.mode != GG_STORE || a.epi != GG_EPI_NONE || a.dr.thr || a.Nsplit < 1 ||
+                  a.N != 2 * a.Nsplit || !a.b2r || !a.b2h || !a.b2dxh || !a.b2part || !gg_ks_wn(a, A16, AKC, BKC)))
+    return fail(GGNN_EINVAL, "gemm: the fused d(rh) epilogue takes the [dX1 | d(rh)] product as a k_gemm_ks launch only");
   if (g_gemm_force != 1 && ring_ok(a, A16, AKC, BKC)) {
     // 32-row tiles for products over one small graph's rows (M <= 64, e.g. the
     // per-(graph, channel) products of v = 30 sentence graphs), and for
@@ -273,25 +300,8 @@ int gg_launch(GemmArgs a, bool A16, bool AKC, bool BKC, int kind, hipStream_t s)
     const dim3 grid((unsigned)nwg);
     Prof p(kind, s);
     const bool sc = a.scA != 1.0f || a.scB != 1.0f || a.snum;
-    // K split over the waves (k_gemm_ks) for one-z products whose 32-row grid
-    // leaves the chip mostly idle and walks >= 8 K slices (the GRU products of a
-    // 20-sentence batch): the narrowest column split whose grid stays within
-    // two workgroups per CU.  (Not for term-listed tiles: over the pair tiles
-    // of a 20-sentence batch 32 x 32 tiles measured slower -- prop_fwd 0.226 ->
-    // 0.249 ms per step, W_c and Y re-read per column block -- and a graph's
-    // channel list would hand the waves other terms under channel skipping,
-    // which must stay bit-identical to the dense loop.)
-    const long kslices = (long)((a.K + 31) / 32) * std::max(a.nterm, 1);
-    int wn = 0;
-    if (!A16 && AKC && !sc && a.tgroups <= 1 && a.Z == 1 && !a.tl) {
-      const int fw = g_gemm_force >= 3 ? 1 << (g_gemm_force - 3) : 0;  // forced: 3 -> WN 1, 4 -> 2, 5 -> 4
-      for (int c = 1; c <= 4 && !fw && small && kslices >= 8 && g_gemm_force != 2; c *= 2)
-        if ((long)((a.M + 31) / 32) * ((a.N + 32 * c - 1) / (32 * c)) <= 512) {
-          wn = c;
-          break;
-        }
-      if (fw) wn = fw;
-    }
+    // K split over the waves: k_gemm_ks (gg_ks_wn)
+    const int wn = gg_ks_wn(a, A16, AKC, BKC);
     if (wn) {
       const int tn32 = (a.N + 32 * wn - 1) / (32 * wn), tm32 = (a.M + 31) / 32;
       const dim3 g32((unsigned)((long)tn32 * tm32));
@@ -594,6 +604,19 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
   // the fast path's k_wgrad256 does (measured <= 3.7e-4 normalised against
   // float64; the dh / dX chain keeps the split limbs): a third of the MFMAs
   constexpr int WPREC = Prec<PREC>::split ? PREC_F16 : PREC;
+  // k_gen_bwd2 fused into the d(rh) product's epilogue when that product is a
+  // k_gemm_ks launch (the small batches), with gbr_rows dbg_r partial rows a
+  // timestep
+  int gbr_rows = 0;
+  {
+    GemmArgs q = gg_args();
+    q.A = P<float>(ws, L.dzc(0)); q.B = P<float>(pack, PL.gWc); q.D = DXH;
+    q.sAm = H; q.sAk = 1; q.sBk = 1; q.sBn = H; q.sDm = 2 * H; q.sDn = 1; q.sD2m = H; q.Nsplit = (int)H;
+    q.M = (int)N; q.N = (int)(2 * H); q.K = (int)H;
+    const int wn = gg_ks_wn(q, false, true, true);
+    if (wn) gbr_rows = (int)((N + 31) / 32) * (4 / wn);
+  }
+  const bool fuse2 = gbr_rows > 0;
   for (int t = c.T - 1; t >= 0; --t) {
     const float* ht = P<float>(ws, L.hsl(t));
     float* DZC = P<float>(ws, L.dzc(t));
@@ -622,9 +645,15 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
       a.D = DXH; a.sDm = 2 * H; a.sDn = 1;
       a.D2 = DRH; a.Nsplit = (int)H; a.sD2m = H;
       a.M = (int)N; a.N = (int)(2 * H); a.K = (int)H;
+      if (fuse2) {
+        // + k_gen_bwd2 in k_gemm_ks's epilogue; dbg_r partials per (32-row
+        // tile, K-slice wave) in GBR
+        a.b2r = G; a.b2h = ht; a.b2dzg = DZG; a.b2dxh = DXH;
+        a.b2part = P<float>(ws, L.GBR) + (size_t)t * gbr_rows * H;
+      }
       if (int e = gg_launch<PREC>(a, false, true, true, K_GRU_BWD, s)) return e;
     }
-    {
+    if (!fuse2) {
       Prof p(K_GRU_BWD, s);
       hipLaunchKernelGGL(k_gen_bwd2, ewg, dim3(256), 0, s, DRH, G, ht, DZG, DXH, N, c.H, gbp);
     }
@@ -822,7 +851,14 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     const int nsl = (int)gen_bias_slices(c);
     // (these sums, and every weight-gradient product's epilogue, GemmArgs::ugmax,
     // carry the unscale 1 / S: no separate pass over the gradients)
-    sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
+    if (fuse2) {
+      // dbg_r from the fused epilogue's rows, dbg_u | dbc from k_gen_bwd1's
+      sp.rows(P<const float>(ws, L.GBR), c.T, gbr_rows, gbr_rows, H, dbg, nullptr, H).ugmax = gmax;
+      sp.add(P<const float>(ws, L.GBP) + H, c.T, nsl, (long)nsl * 3 * H, 3 * H, 2 * H, 2 * H, 0, dbg + H, dbc, H)
+          .ugmax = gmax;
+    } else {
+      sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
+    }
     sp.launch(s);
     if (c.sparse && use_bias) {
       GemmArgs r = gg_args();

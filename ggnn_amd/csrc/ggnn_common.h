@@ -353,6 +353,8 @@ DEV float drop_apply(const Drop& d, uint32_t w, float x) { return w < d.thr ? x 
 // the GRU state update h' = u h + (1 - u) c with one rounding order wherever
 // it is formed (k_gen_blend, k_gemm_ks's fused epilogue)
 DEV float gru_blend(float u, float h, float c) { return __builtin_fmaf(u, h, (1.0f - u) * c); }
+// dzg_r = d(rh) h r (1 - r) (k_gen_bwd2, k_gemm_ks's fused epilogue)
+DEV float gru_dzg_r(float x, float h, float r) { return x * h * r * (1.0f - r); }
 
 // ---- backward gradient scaling.  The btb loss is divided by the number of
 // targets (chem_tensorflow.py:360,399-403), so dL/dh_T arrives at ~1/b per

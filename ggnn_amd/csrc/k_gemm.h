@@ -126,6 +126,16 @@ struct GemmArgs {
   const float* bu;
   int bv, bt;
   Drop bsd;
+  // if set (the product [dX1 | d(rh)] = dzc Wc^T, Nsplit = H): k_gen_bwd2 on
+  // the d(rh) columns n >= H (k = n - H), x = d(rh), r = b2r[m * 2H + k],
+  // h = b2h[m * H + k]: b2dzg[m * 2H + k] = x h r (1 - r), b2dxh[m * 2H + H + k]
+  // += x r, and the dbg_r partial of each wave's rows in b2part[(32-row tile *
+  // WK + wk) * H + k] (k_gemm_ks only)
+  const float* b2r;
+  const float* b2h;
+  float* b2dzg;
+  float* b2dxh;
+  float* b2part;
   // -DGGNN_TS experiment builds: k + 1 = record this launch's per-workgroup
   // phase stamps in g_ts[k] (tools/ts_probe_generic.py); 0 = none
   int tsprobe;

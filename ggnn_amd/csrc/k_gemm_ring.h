@@ -721,6 +721,22 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
       pre2[e] = a.bu[row * 2 * a.N + a.N + n];
     }
   }
+  // the fused k_gen_bwd2 (GemmArgs::b2dzg) on the d(rh) columns: r, h and
+  // the dh half of DXH loaded up front
+  const bool b2n = a.b2dzg && hi_n;
+  const int k2 = n - a.Nsplit;
+  const long H2 = 2L * a.Nsplit;
+  float pr[16 / WK], ph[16 / WK], pd[16 / WK];
+  if (b2n) {
+#pragma unroll
+    for (int e = 0; e < 16 / WK; ++e) {
+      const long row = min(m0 + acc_row(4 * (wk * (4 / WK) + (e >> 2)), hh) + (e & 3), a.M - 1);
+      pr[e] = a.b2r[row * H2 + k2];
+      ph[e] = a.b2h[row * a.Nsplit + k2];
+      pd[e] = a.b2dxh[row * H2 + a.Nsplit + k2];
+    }
+  }
+  float s2 = 0.f;
   const Drop sd = bln ? drop_resolve(a.bsd) : Drop{};
   long wkey = -1;  // the first row of the state-dropout quad whose words w holds
   uint4 sw = make_uint4(0u, 0u, 0u, 0u);
@@ -761,6 +777,12 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
         }
         a.bout[(long)m * a.N + n] = y;
       }
+      if (b2n) {
+        const float r = pr[4 * qq + r4], zr = gru_dzg_r(x, ph[4 * qq + r4], r);
+        a.b2dzg[(long)m * H2 + k2] = zr;
+        a.b2dxh[(long)m * H2 + a.Nsplit + k2] = __builtin_fmaf(x, r, pd[4 * qq + r4]);
+        s2 += zr;
+      }
       if (dr.thr) x = drop_apply(dr, u4_get(dq, r4), x);
       const long doff = dn + (long)m * sm;
       if (a.E) x *= pre[4 * qq + r4];
@@ -776,5 +798,9 @@ __global__ void __launch_bounds__(256, 2) k_gemm_ks(GemmArgs a, int tm, int tn) 
   if (a.csum) {
     cs += __shfl_xor(cs, 32);
     if (hh == 0) atomicAdd(a.csum + (long)zp * a.scp + (long)zq * a.scq + n, cs);  // (k_gemm_ks: no cpart callers)
+  }
+  if (b2n) {
+    s2 += __shfl_xor(s2, 32);
+    if (hh == 0) a.b2part[((long)mt * WK + wk) * a.Nsplit + k2] = s2;
   }
 }

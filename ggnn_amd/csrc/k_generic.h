@@ -229,9 +229,9 @@ __global__ void __launch_bounds__(256) k_gen_bwd2(const float* __restrict__ drh,
   for (long row = r0; row < r1; ++row) {
     const long e = row * H + k;
     const float r = G[row * 2 * H + k], x = drh[e];
-    const float zr = x * h[e] * r * (1.0f - r);
+    const float zr = gru_dzg_r(x, h[e], r);
     dzg[row * 2 * H + k] = zr;
-    DXH[row * 2 * H + H + k] += x * r;
+    DXH[row * 2 * H + H + k] = __builtin_fmaf(x, r, DXH[row * 2 * H + H + k]);
     sr += zr;
   }
   bpart[(long)blockIdx.y * 3 * H + k] = sr;
