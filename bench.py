@@ -10,7 +10,9 @@ and all six weight gradients) [+ one RCCL all-reduce of the flat gradient
 buffer when N > 1] + the reference's optimizer update of the six variables
 (per-tensor clip_by_norm + TF1 Adam, chem_tensorflow.py:494-503).
 Weak scaling: every rank owns its own 256-graph batch; value = N*256 / t_step
-with t_step the max over ranks.
+with t_step the max over ranks.  Beside it (strong_scaling): one global batch
+of 256 graphs split 256/N per rank, timed the same way; the per-step
+all-reduce's time and bus bandwidth and the min / max rank step time.
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W]
       N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set)
@@ -272,6 +274,54 @@ def precision_error(dev, precision, host, T):
     return out
 
 
+def gru_inference_leg(eng, h0_d, w_d, A_d, b, v, h, C, T, precision, steps=10):
+    """The unfused forward in inference mode (training=False: no saves for the
+    backward), k_gru_fwd timed per launch with HIP events.  SURVEY §8(d)'s GRU
+    bytes -- X, h in + h' out, fp32: 12 v h per graph-step -- are the contract
+    north_star's ">= 50 % of HBM peak on the fused GRU" is quoted on (25.2 us
+    per timestep at config 3); traffic: PMC bytes per launch of the same
+    inference-only launches (tools/gru_infer_probe.py under rocprofv3 --pmc,
+    profiles/pmc_traffic_<precision>_infer.json)."""
+    import torch
+    from ggnn_amd import _lib
+    out = torch.empty((b, v, h), dtype=torch.float32, device=h0_d.device)
+    pack = eng.pack_weights(w_d, T=T)
+    eng.set_adjacency(A_d)
+
+    def fwd():
+        eng.forward(h0_d, pack, T, training=False, out=out)
+
+    ms = _timed_events(fwd, steps)
+    timer = _lib.KernelTimer(max_launches=50 * steps)
+    with timer:
+        for _ in range(steps):
+            fwd()
+        torch.cuda.synchronize()
+    res = {"ms_per_forward": ms, "graphs_per_s": b / (ms * 1e-3), "kernels": {}}
+    tr = load_traffic(precision + "_infer") or {}
+    for k in ("prop_fwd", "gru_fwd"):
+        if not timer.launches.get(k):
+            continue
+        avg = timer.total_ms[k] / timer.launches[k]
+        fl = kernel_algo_flops(k, b, v, h, C, T)
+        d = {"avg_launch_ms": avg, "launches_per_forward": timer.launches[k] / steps,
+             "frac_of_bf16_peak": fl / (avg * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+        if k == "gru_fwd":
+            ab = 12 * v * h * b
+            d.update(algorithmic_bytes_per_launch=ab,
+                     frac_of_hbm_peak_algorithmic=ab / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     north_star_us_per_timestep_at_half_peak=ab / (0.5 * HBM_PEAK_GBS * 1e9) * 1e6)
+        kt = tr.get("kernels", {}).get(k)
+        if kt:
+            gbs = kt["hbm_bytes_per_launch"] / (avg * 1e-3) / 1e9
+            d.update(traffic=kt["hbm_bytes_per_launch"], hbm_read_bytes=kt["hbm_read_bytes"],
+                     hbm_write_bytes=kt["hbm_write_bytes"], hbm_gbs=gbs, frac_of_hbm_peak=gbs / HBM_PEAK_GBS,
+                     frac_roofline=max(d["frac_of_bf16_peak"], gbs / HBM_PEAK_GBS),
+                     traffic_source="profiles/pmc_traffic_%s_infer.json" % precision)
+        res["kernels"][k] = d
+    return res
+
+
 def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10, unfused=False, host=None):
     """The same fwd+bwd step in a reduced-precision mode (single 16-bit MFMA
     operands): graphs/s and the prop kernels' fraction of the dense bf16 MFMA
@@ -326,12 +376,15 @@ def precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps=10,
             fr[k] = d
     out = {"precision": precision, "value": b / (ms * 1e-3), "unit": "graphs/s", "ms_per_step": ms,
            "step": "pack + adjacency + fwd + bwd (no optimizer)", "kernels": fr}
+    if unfused:
+        out["inference"] = gru_inference_leg(eng, h0_d, w_d, A_d, b, v, h, C, T, precision, steps)
     if host is not None:
         out["error_vs_float64"] = precision_error(dev, precision, host, T)
     if not unfused:
         u = precision_side(dev, precision, A_d, h0_d, w_d, dhT, b, v, h, C, T, steps, unfused=True)
         out["unfused_forward"] = {"value": u["value"], "ms_per_step": u["ms_per_step"],
                                   "kernels": {k: u["kernels"][k] for k in ("prop_fwd", "gru_fwd") if k in u["kernels"]},
+                                  "inference": u["inference"],
                                   "note": "the forward as per-timestep k_prop_fwd + k_gru_fwd launches "
                                           "(GGNN_UNFUSED_FWD): north_star's adj x h (>= 30 % of bf16 MFMA peak) "
                                           "and fused-GRU (>= 50 % of HBM peak) targets are quoted on these kernels"}
@@ -638,23 +691,88 @@ def spawn_ranks(n: int, argv, timeout_s: float | None = None) -> int:
     return rc
 
 
+def strong_batch(world: int) -> int:
+    """Per-rank batch of the strong-scaling leg: the
+    global batch of configs[2] (256 graphs) split evenly over the ranks."""
+    if CFG["b"] % world:
+        raise SystemExit("bench.py: the strong-scaling leg splits b=%d over %d ranks evenly" % (CFG["b"], world))
+    return CFG["b"] // world
+
+
+def rank_spread(vals, dev=None):
+    """(max, min) over the ranks of each value in `vals` (one MAX all-reduce
+    of [x, -x]); the values themselves outside a process group."""
+    import torch
+    import torch.distributed as tdist
+    if not tdist.is_initialized():
+        return list(vals), list(vals)
+    t = torch.tensor(list(vals) + [-x for x in vals], dtype=torch.float64, device=dev)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    n = len(vals)
+    t = t.cpu().tolist()
+    return t[:n], [-x for x in t[n:]]
+
+
+def all_reduce_costs(flat, reps, on_gpu=True):
+    """The gradient all-reduce alone: `reps` back-to-back all-reduces of the
+    flat gradient buffer after a barrier, timed with a HIP event pair on the
+    stream torch.distributed makes wait for the collective (RCCL runs it on
+    its own stream; the current stream's events bracket its completion), or
+    with the host clock for gloo on CPU tensors.  Bus bandwidth as RCCL's
+    tests define it for a ring all-reduce: 2 (N-1)/N S / t.  Max over ranks."""
+    import torch
+    import torch.distributed as tdist
+    from ggnn_amd.dist import _reducing
+    if not _reducing(None):
+        return None
+    world = tdist.get_world_size()
+    tdist.all_reduce(flat)                        # warm-up (communicator setup)
+    tdist.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            tdist.all_reduce(flat)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+    else:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tdist.all_reduce(flat)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+    (ms_max,), (ms_min,) = rank_spread([ms], flat.device if on_gpu else None)
+    S = flat.numel() * flat.element_size()
+    return {"isolated_ms_per_call": ms_max, "isolated_ms_per_call_min_rank": ms_min, "reps": reps,
+            "bytes": S, "bus_bandwidth_gbs": 2.0 * (world - 1) / world * S / (ms_max * 1e-3) / 1e9 if world > 1
+            else None, "algo_bandwidth_gbs": S / (ms_max * 1e-3) / 1e9}
+
+
 def launch_rehearsal(args):
     """--launch-only: the N-rank launch and its process group without the
     propagation step (no GPU work, runs on CPU with --dist-backend gloo): every
-    rank joins the group and all-reduces its rank's batch size; rank 0 prints
-    one JSON line with the world size and global batch the bench line would
-    carry.  It is not a measurement (no metric, no value)."""
+    rank joins the group and all-reduces its rank's batch of the weak leg and
+    of the strong leg, then times the all-reduce of a CPU buffer the size of
+    the flat gradient buffer (all_reduce_costs, host clock); rank 0 prints one
+    JSON line with the world size, the global batches and the keys the bench
+    line carries.  It is not a measurement of the path (no metric, no value)."""
     import torch
     import torch.distributed as tdist
-    from ggnn_amd.dist import init_from_env
+    from ggnn_amd.dist import grad_shapes, init_from_env
     rank, world, _ = init_from_env(args.dist_backend)
-    b = torch.tensor([float(CFG["b"])])
+    bs = strong_batch(world)
+    b = torch.tensor([float(CFG["b"]), float(bs)])
     if tdist.is_initialized():
         tdist.all_reduce(b)
+    n = sum(int(np.prod(s)) for s in grad_shapes(CFG["h"], 2 * CFG["e"]).values())
+    ar = all_reduce_costs(torch.zeros(n), reps=5, on_gpu=False) if tdist.is_initialized() else None
     if rank == 0:
         print(json.dumps({"launch_rehearsal": True, "n_gpus": world, "world_size": world,
-                          "config": {"global_batch": int(b.item()), "parallelism": "dp%d" % world},
-                          "all_reduce": {"backend": tdist.get_backend() if tdist.is_initialized() else None},
+                          "config": {"global_batch": int(b[0].item()), "parallelism": "dp%d" % world},
+                          "strong_scaling": {"per_rank_batch": bs, "global_batch": int(b[1].item())},
+                          "all_reduce": dict(ar or {}, backend=tdist.get_backend() if tdist.is_initialized()
+                                             else None),
                           "pid": os.getpid(), "launcher": os.environ.get("GGNN_BENCH_LAUNCHER", "external")}),
               flush=True)
     if tdist.is_initialized():
@@ -739,60 +857,89 @@ def main():
     out = torch.empty((b, v, h), dtype=torch.float32, device=dev)
 
     nstep = [0]
+    ar_events = []          # (start, end) event pairs around the in-step all-reduce (instrumented pass)
 
-    def step(keep=1.0):
-        # keep < 1: the reference's training feed (edge-weight + state dropout,
-        # chem_tensorflow_dense.py:860-861), a fresh Philox seed every step
-        nstep[0] += 1
-        pack = eng.pack_weights(w_d, T=T, edge_keep=keep, seed=nstep[0])
-        eng.set_adjacency(A_d)
-        eng.forward(h0_d, pack, T, training=True, out=out, state_keep=keep)
-        eng.backward(dhT, gviews)
-        grads.all_reduce()
-        opt.step([grads.views[k] for k in GRAD_ORDER], grad_scale=1.0 / world)
+    def make_step(eng_, A_, h0_, dhT_, gviews_, grads_, out_):
+        def step(keep=1.0, ev=None):
+            # keep < 1: the reference's training feed (edge-weight + state dropout,
+            # chem_tensorflow_dense.py:860-861), a fresh Philox seed every step
+            nstep[0] += 1
+            pack = eng_.pack_weights(w_d, T=T, edge_keep=keep, seed=nstep[0])
+            eng_.set_adjacency(A_)
+            eng_.forward(h0_, pack, T, training=True, out=out_, state_keep=keep)
+            eng_.backward(dhT_, gviews_)
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                grads_.all_reduce()
+                e1.record()
+                ev.append((e0, e1))
+            else:
+                grads_.all_reduce()
+            opt.step([grads_.views[k] for k in GRAD_ORDER], grad_scale=1.0 / world)
+        return step
+
+    step = make_step(eng, A_d, h0_d, dhT, gviews, grads, out)
 
     def barrier():
         if tdist.is_initialized():
             tdist.barrier()
         torch.cuda.synchronize()
 
+    def timed(fn, n, *a):
+        barrier()
+        t_ = time.perf_counter()
+        for _ in range(n):
+            fn(*a)
+        barrier()
+        return (time.perf_counter() - t_) / n
+
     for _ in range(args.warmup):
         step()
     barrier()
     # timed region: exactly K steps, nothing else on the stream
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    t1 = time.perf_counter()
-    dt = (t1 - t0) / args.steps
+    dt = timed(step, args.steps)
     # the same K steps again with a HIP event pair around every library launch
     # (kernel durations for the roofline; the events add gaps between launches,
-    # so this pass is not the headline time)
+    # so this pass is not the headline time) and around the all-reduce
     timer = _lib.KernelTimer(max_launches=200 * max(args.steps, 1))
     with timer:
-        barrier()
-        t3 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        barrier()
-        dt_instr = (time.perf_counter() - t3) / args.steps
+        dt_instr = timed(step, args.steps, 1.0, ar_events)
     # the same step with the training-feed dropout (keep 0.9 for both), reported beside
     dt_drop = float("nan")
     if not args.no_dropout_leg:
         for _ in range(args.warmup):
             step(args.dropout_keep)
-        barrier()
-        t2 = time.perf_counter()
-        for _ in range(args.steps):
-            step(args.dropout_keep)
-        barrier()
-        dt_drop = (time.perf_counter() - t2) / args.steps
-    if tdist.is_initialized():
-        tt = torch.tensor([dt, dt_drop], dtype=torch.float64, device=dev)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        dt, dt_drop = float(tt[0].item()), float(tt[1].item())
+        dt_drop = timed(step, args.steps, args.dropout_keep)
+    # strong scaling: the global batch of 256 graphs split
+    # 256/N per rank, timed exactly like the weak leg.  At N = 1 it IS the weak leg.
+    bs = strong_batch(world)
+    dt_strong = dt
+    if world > 1:
+        # rank r takes graphs [r*bs, (r+1)*bs) of ONE global batch (rank 0's seed)
+        As, h0s = (A, h0) if rank == 0 else O.synthetic_batch(b, v, h, C, seed=1)
+        sl = slice(rank * bs, (rank + 1) * bs)
+        As_d = torch.from_numpy(np.ascontiguousarray(As[sl])).to(dev)
+        h0s_d = torch.from_numpy(np.ascontiguousarray(h0s[sl])).to(dev)
+        eng_s = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision)
+        grads_s = FlatGradients(h, C, True, device=dev)
+        gv_s = dict(grads_s.views)
+        gv_s["h0"] = torch.empty((bs, v, h), dtype=torch.float32, device=dev)
+        out_s = torch.empty((bs, v, h), dtype=torch.float32, device=dev)
+        step_s = make_step(eng_s, As_d, h0s_d, dhT[sl].contiguous(), gv_s, grads_s, out_s)
+        for _ in range(args.warmup):
+            step_s()
+        dt_strong = timed(step_s, args.steps)
+        del eng_s, grads_s, gv_s, out_s, As_d, h0s_d
+        torch.cuda.empty_cache()
+    ar_in_step = None
+    from ggnn_amd.dist import _reducing
+    if ar_events and _reducing(None):
+        torch.cuda.synchronize()
+        ar_in_step = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ar_events]))
+    ar_iso = all_reduce_costs(grads.flat, reps=max(args.steps, 10))
+    (dt, dt_drop, dt_strong, dt_instr, ar_max), (dt_min, dt_drop_min, dt_strong_min, _, ar_min) = rank_spread(
+        [dt, dt_drop, dt_strong, dt_instr, ar_in_step if ar_in_step is not None else float("nan")], dev)
 
     if args.pmc_unfused_leg:
         ueng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision,
@@ -904,10 +1051,25 @@ def main():
             "roofline": roof,
             "achieved_step_tflops": world * b * fpg / dt / 1e12,
             "kernel_breakdown": breakdown,
-            "all_reduce": {"backend": tdist.get_backend() if tdist.is_initialized() else None,
+            "rank_step_ms": {"max": dt * 1e3, "min": dt_min * 1e3,
+                             "note": "each rank's K-step average; value uses the max (the slowest rank)"},
+            "strong_scaling": {"value": b / dt_strong, "unit": "graphs/s", "ms_per_step": dt_strong * 1e3,
+                               "ms_per_step_min_rank": dt_strong_min * 1e3, "per_rank_batch": bs,
+                               "global_batch": b, "scaling": "strong",
+                               "note": "global batch of 256 graphs split 256/N per rank (SURVEY §8d, config 4), "
+                                       "same step and timing as the weak value; at N = 1 the weak leg itself"},
+            "all_reduce": dict(ar_iso or {}, **{
+                           "backend": tdist.get_backend() if tdist.is_initialized() else None,
                            "bytes_per_step": grads.nbytes,
+                           "in_step_ms": None if np.isnan(ar_max) else ar_max,
+                           "in_step_ms_min_rank": None if np.isnan(ar_min) else ar_min,
+                           "in_step_bus_bandwidth_gbs": (2.0 * (world - 1) / world * grads.nbytes / (ar_max * 1e-3)
+                                                         / 1e9) if world > 1 and not np.isnan(ar_max) else None,
                            "note": "one all-reduce of the flat fp32 gradient buffer per step (RCCL = backend "
-                                   "nccl); none without a process group"},
+                                   "nccl); none without a process group.  in_step_ms: HIP events on the step's "
+                                   "stream around the collective in the instrumented pass (includes waiting for "
+                                   "the slowest rank); isolated_ms_per_call: back-to-back all-reduces after a "
+                                   "barrier; bus bandwidth 2(N-1)/N S / t"}),
             "launcher": os.environ.get("GGNN_BENCH_LAUNCHER", "external (torch.distributed.run)"
                                        if "WORLD_SIZE" in os.environ else "single process"),
             "ms_per_step_event_instrumented": dt_instr * 1e3,

@@ -722,7 +722,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
         SumJob& q = sp.add(a.cpart, (int)c.b, (int)S, C * S * H, H, C * H, H, S * H, dbeta, dbeta, C * H, 1);
         q.ugmax = gmax;
         if (!dense_ch) { q.mask = P<const unsigned char>(adj, AL.occ); q.mT = C; q.mC = 1; }
-        sp.launch(s);
+        if (int e = sp.launch(s)) return e;
       }
     }
     // dh[g] += sum over g's channels of dM[g,c] W_c^T
@@ -859,7 +859,7 @@ int gen_backward(const Cfg& c, const void* pack, void* adj, void* ws, const floa
     } else {
       sp.rows(P<const float>(ws, L.GBP), c.T, nsl, nsl, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
     }
-    sp.launch(s);
+    if (int e = sp.launch(s)) return e;
     if (c.sparse && use_bias) {
       GemmArgs r = gg_args();
       r.slab = P<float>(ws, L.PDB); r.sSlab = H; r.D = dbeta; r.sDm = 0; r.M = 1; r.N = (int)H;

@@ -226,16 +226,21 @@ AdjL adj_layout(const Cfg& c) {
 struct WsL {
   size_t hb[2], Xa, hf[2];        // state (fp32 master; bf16 operand copy in bf16 mode)
   size_t hfT, hT, XT, rhT, r, u, c;  // saved per step (training)
-  size_t dA, dB, dXT, dzcT, dzgT, dMT, G, dbp, gmax, wpart, gbp, sump;
+  size_t dA, dB, dXT, dzcT, dzgT, dMT, dbp, gmax, wpart, gbp, sump, sbits;
   size_t nh4, nha, nhw;            // bytes of one [N][H] fp32 / activation / wgrad-operand array
   size_t total;
 };
 // the weight-gradient launch's plan (k_wgrad / k_wgrad256): output tile size,
-// K chunk, tiles (incl. the per-timestep dW tiles under edge dropout) and the
-// tiles of T-summed problems the chunk count is sized by
+// K chunk and chunk count of the T-summed problems, tiles, and -- under edge
+// dropout -- the dW problem's timestep-aligned chunks: cpt chunks of KCt rows
+// per timestep, each inside ONE timestep, so k_wgrad_reduce can apply the
+// timestep's mask to the sum of its chunks (round 6: replaces the per-timestep
+// dW tiles, their fp32 G scratch and k_edge_mask_reduce)
 struct WgPlan {
   int TS;
-  long KC, nchunks, tiles, tiles_eq;
+  long KC, nchunks, tiles;
+  long cpt, KCt;  // edge dropout only (else 0)
+  long wgs;       // workgroups of the launch = partial tiles in the workspace
 };
 long wg256_kc(const Cfg& c);
 WgPlan wg_plan(const Cfg& c) {
@@ -244,17 +249,29 @@ WgPlan wg_plan(const Cfg& c) {
   const bool big = H == 256 && N % 128 == 0;
   w.TS = big ? 256 : 128;
   const long t2 = (H / w.TS) * (H / w.TS);
-  w.tiles_eq = (6 + c.C) * t2;
-  w.tiles = (6 + (c.ed ? (long)c.T * c.C : c.C)) * t2;
+  w.tiles = (6 + c.C) * t2;
   if (big) {
     w.KC = wg256_kc(c);
   } else {
     long KC = 4096;
     while (KC > 32 && (N % KC) != 0) KC /= 2;
-    while (KC > 256 && w.tiles_eq * (N / KC) < 256) KC /= 2;
+    while (KC > 256 && w.tiles * (N / KC) < 256) KC /= 2;
     w.KC = KC;
   }
   w.nchunks = std::max<long>(N / std::max<long>(w.KC, 1), 1);
+  w.cpt = w.KCt = 0;
+  long dw_chunks = w.nchunks;
+  if (c.ed) {
+    // about as many chunks as the T-summed problems have (the same work per
+    // workgroup): the smallest power of two >= nchunks / T whose chunk is a
+    // whole number of 32-row slices, else one chunk per timestep
+    long cpt = 1;
+    while (cpt * c.T < w.nchunks && N % (cpt * 2 * 32) == 0) cpt *= 2;
+    w.cpt = cpt;
+    w.KCt = N / cpt;
+    dw_chunks = (long)c.T * cpt;
+  }
+  w.wgs = 6 * t2 * w.nchunks + (long)c.C * t2 * dw_chunks;
   return w;
 }
 // rows of k_gru_bwd's per-workgroup bias partials (one row per (timestep, workgroup))
@@ -263,14 +280,21 @@ constexpr int SUM_RCS = 32;  // k_sum_rows' row chunks (at most)
 // Builder of one k_sum_rows / k_sum_rows_fin pair (fixed-order column sums):
 // jobs take consecutive pieces of the scratch at `scr` (SUM_RCS * E floats
 // each at most)
+static_assert(GGNN_MAX_HEADS <= SUMJ_MAX, "heads_backward adds one SumPlan job per head");
 struct SumPlan {
   SumJobs sj;
   int nb = 0, nf = 0;
   float* scr;
+  bool full = false;  // a job past SUMJ_MAX was refused (launch() then fails)
+  SumJob spill;       // what a refused add() hands back (never launched)
   explicit SumPlan(float* scratch) : scr(scratch) { memset(&sj, 0, sizeof(sj)); }
   // rows (t, w): part + t * sT + w * sW + (e / Nc) * sC + e % Nc
   SumJob& add(const float* part, int T, int nw, long sT, long sW, long E, long Nc, long sC, float* o0, float* o1,
               long split, int accumulate = 0) {
+    if (sj.count == SUMJ_MAX) {
+      full = true;
+      return spill;
+    }
     SumJob& q = sj.j[sj.count];
     const long rows = (long)T * nw;
     q.part = part; q.T = T; q.nw = nw; q.sT = sT; q.sW = sW; q.E = E; q.Nc = Nc; q.sC = sC;
@@ -288,12 +312,15 @@ struct SumPlan {
   SumJob& rows(const float* part, int T, int nw, long stride, long E, float* o0, float* o1, long split) {
     return add(part, T, nw, stride * E, E, E, E, 0, o0, o1, split);
   }
-  void launch(hipStream_t s) {
-    if (!sj.count) return;
+  // GGNN_OK, or an error (nothing launched) when more than SUMJ_MAX jobs were added
+  int launch(hipStream_t s) {
+    if (full) return fail(GGNN_EINVAL, "k_sum_rows: more than " + std::to_string(SUMJ_MAX) + " sum jobs");
+    if (!sj.count) return GGNN_OK;
     sj.bx[sj.count] = nb;
     sj.fx[sj.count] = nf;
     hipLaunchKernelGGL(k_sum_rows, dim3(nb), dim3(256), 0, s, sj);
     hipLaunchKernelGGL(k_sum_rows_fin, dim3(nf), dim3(256), 0, s, sj);
+    return GGNN_OK;
   }
 };
 // k_slab_reduce over groups of z (GemmArgs::slab)
@@ -334,6 +361,13 @@ void slab_reduce_t(const GemmArgs& a, int G, const int* zs, int zsdiv, int nt, l
   else hipLaunchKernelGGL(k_seg_reduce<1>, dim3((unsigned)((n + 3) / 4), (unsigned)G), dim3(256), 0, s, r);
 }
 
+// the whole T-step forward of each graph in one workgroup (k_fused.h)
+bool fused_fwd(const Cfg& c) {
+  return !c.generic && c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT && !(c.flags & GGNN_UNFUSED_FWD);
+}
+// training under state dropout on the fused forward: it writes the keep bits of
+// every timestep's state mask (FusedFwdArgs::sbits), which the backward reads
+bool state_bits(const Cfg& c) { return c.sd && fused_fwd(c); }
 WsL ws_layout(const Cfg& c, bool training) {
   WsL L;
   memset(&L, 0, sizeof(L));
@@ -365,15 +399,19 @@ WsL ws_layout(const Cfg& c, bool training) {
     L.dzcT = o; o += L.nhw * T;
     L.dzgT = o; o += 2 * L.nhw * T;
     L.dMT = o;  o += C * L.nhw * T;
-    if (c.ed) { L.G = o; o += al(T * C * H * H * 4); }  // per-timestep dW (edge dropout)
     L.dbp = o; o += al(T * (size_t)c.b * C * H * 4);    // per-(timestep, graph) dL/dbeta partials
     L.gmax = o; o += al(GMAX_BYTES);                      // max |dL/dh_T| (gradient scale, ggnn_common.h) + k_absmax partials
     if (H >= 128) {                                       // deterministic K-chunk reduction of the weight gradients
       const WgPlan w = wg_plan(c);
-      L.wpart = o; o += al((size_t)w.tiles * w.nchunks * w.TS * w.TS * 4);
+      L.wpart = o; o += al((size_t)w.wgs * w.TS * w.TS * 4);
     }
     L.gbp = o; o += al((size_t)gru_bias_rows(c) * 3 * H * 4);  // k_gru_bwd's [dbg | dbc] partials
     L.sump = o; o += al((size_t)SUM_RCS * (3 * H + C * H) * 4);  // k_sum_rows' per-row-chunk sums
+    // the state keep bits [T][b][512 threads] uint2 (state_bits): laid out
+    // whenever the fused forward runs, whatever the keep probabilities, so a
+    // workspace sized without state dropout still holds them (5 MiB at config 3)
+    L.sbits = 0;
+    if (fused_fwd(c)) { L.sbits = o; o += al((size_t)T * c.b * 512 * 8); }
   }
   L.total = o;
   return L;
@@ -456,19 +494,21 @@ long wg256_kc(const Cfg& c) {
 // k_prop_bwd writes no dM^T rows for a graph's empty channels.
 bool wgrad_lists(const Cfg& c) {
   if (!(c.H == 256 && c.N % 128 == 0) || (c.flags & GGNN_DENSE_CHANNELS)) return false;
-  const long KC = wg256_kc(c), nchunks = c.N / KC;
-  return (c.b + nchunks - 1) / nchunks <= WG_LIST_MAX && c.V % 32 == 0;
+  const WgPlan w = wg_plan(c);
+  const long per_t = c.ed ? w.cpt : w.nchunks;  // chunks a channel's graph list is split into
+  return (c.b + per_t - 1) / per_t <= WG_LIST_MAX && c.V % 32 == 0;
 }
 
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, ChanL chl,
                      const PackL& PL, const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp,
-                     const uint32_t* gmax, hipStream_t s) {
+                     const uint32_t* gmax, const uint2* sbits, hipStream_t s) {
   Prof p(K_PROP_BWD, s);
+  // (the forward's state keep bits: 128-row graphs at hidden 256 only)
   hipLaunchKernelGGL((k_prop_bwd<V, H, PREC>), dim3(c.b), dim3(2 * H), 0, s, (const ActT<PREC>*)dXT, AbT, deg, chl.p,
                      chl.stride,
                      P<u16>(pk, PL.wt(c.ed ? t : 0)), PL.loW, dh_in, dh_out, (u16*)dMT, dbp, c.C, c.N, c.sdrop, t - 1,
-                     gmax, (int)!wgrad_lists(c));
+                     gmax, (int)!wgrad_lists(c), (V == 128 && H == 256) ? sbits : (const uint2*)nullptr);
 }
 template <int H, int RT, int PREC>
 void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const float* hf, const PackL& PL,
@@ -491,12 +531,13 @@ void launch_gru_fwd(const Cfg& c, int t, const void* Xa, const u16* hb, const fl
 template <int H, int RT, int PREC>
 void launch_gru_bwd(const Cfg& c, const float* delta, const float* hf, const float* r, const float* u, const float* cc,
                     const PackL& PL, const void* pk, void* dXT, float* dh_out, void* dzcT, void* dzgT, float* dbc,
-                    float* dbg, const uint32_t* gmax, float* bpart, int* nwg, hipStream_t s) {
+                    float* dbg, const uint32_t* gmax, float* bpart, const uint2* sbits, int* nwg, hipStream_t s) {
   Prof p(K_GRU_BWD, s);
   *nwg = (int)(c.N / (32 * RT));
   hipLaunchKernelGGL((k_gru_bwd<H, RT, PREC>), dim3(c.N / (32 * RT)), dim3(2 * H), 0, s, delta, hf, r, u, cc,
                      P<u16>(pk, PL.WcT), P<u16>(pk, PL.WgT), PL.loWc, PL.loWg, (ActT<PREC>*)dXT, dh_out,
-                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N, gmax, bpart);
+                     (u16*)dzcT, (u16*)dzgT, dbc, dbg, c.N, gmax, bpart,
+                     (H == 256 && c.V == 128) ? sbits : (const uint2*)nullptr, c.sdrop.scale);
 }
 long gru_bias_rows(const Cfg& c) { return (long)c.T * std::max<long>(c.N / 32, 1); }
 
@@ -535,10 +576,6 @@ struct launch_gru_bwd_tag {};
 template <typename TAG, int H> struct kMaxRT { static constexpr int value = 4; };
 template <typename TAG> struct kSplitRT { static constexpr int value = 2; };
 template <> struct kMaxRT<launch_gru_bwd_tag, 256> { static constexpr int value = 2; };
-#ifndef GGNN_GB_MAXRT
-#define GGNN_GB_MAXRT 2
-#endif
-template <> struct kSplitRT<launch_gru_bwd_tag> { static constexpr int value = GGNN_GB_MAXRT; };
 
 void launch_pack(bool f16, const float* S, int ldS, long sS, int K, int N, int trans, u16* out, long sO, long lo,
                  int batch, hipStream_t s, Drop dr = Drop{0, 0, 0, 1.0f}, int t = 0) {
@@ -569,7 +606,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
   // may have changed)
   const bool dense = c.vin == c.V;
   // the whole T-step forward of each graph in one workgroup (k_fused.h)
-  const bool fused = c.H == 256 && c.V == 128 && c.T <= FUSED_MAXT && !(c.flags & GGNN_UNFUSED_FWD);
+  const bool fused = fused_fwd(c);
   float* hf0 = tr ? P<float>(ws, L.hfT) : P<float>(ws, L.hf[0]);
   if (tr) {
     Prof p(K_IO, s);
@@ -617,6 +654,7 @@ int forward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, bool
     fa.T = c.T;
     fa.vsh = c.vsh;
     fa.sd = c.sdrop;
+    fa.sbits = (tr && state_bits(c)) ? P<uint2>(ws, L.sbits) : nullptr;
     {
       Prof p(K_FWD_FUSED, s);
       hipLaunchKernelGGL(k_fwd_fused<PREC>, dim3(c.b), dim3(512), 0, s, fa);
@@ -685,8 +723,8 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   const bool use_bias = (c.flags & GGNN_USE_EDGE_BIAS) != 0;
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
 
-  // (the weight and bias gradients need no clearing: k_wgrad_reduce,
-  // k_edge_mask_reduce and k_sum_rows store every element once)
+  // (the weight and bias gradients need no clearing: k_wgrad_reduce and
+  // k_sum_rows store every element once)
   // gradient scale: the backward runs on S * dL/dh_T, S = 2^-floor(log2 max|dL/dh_T|),
   // and divides its outputs by S (ggnn_common.h gscale): loss-normalised
   // gradients (~1/b) stay inside the f16 limbs' normal range
@@ -700,7 +738,10 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
   // unpadded batch without state dropout: dL/dh_T is read in place and the
   // last step writes dL/dh0 in place
   const bool dense = c.vin == c.V;
-  const bool in_place = dense && !c.sd;
+  // the forward's state keep bits (state_bits): the first step applies the
+  // last timestep's mask to dL/dh_T as it reads it, so it is read in place too
+  const uint2* sb = state_bits(c) ? P<const uint2>(ws, L.sbits) : nullptr;
+  const bool in_place = dense && (!c.sd || sb);
   if (!in_place) {
     Prof p(K_IO, s);
     hipLaunchKernelGGL(k_pad_state, dim3(grid1d(N / 4 * H)), dim3(256), 0, s, dhT, c.vin, c.V, c.H, dA, (u16*)nullptr, N, 0,
@@ -716,22 +757,17 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
                  P<float>(ws, L.u + L.nh4 * t), P<float>(ws, L.c + L.nh4 * t), PL, pack, P<void>(ws, L.dXT), dB,
                  P<void>(ws, L.dzcT + L.nhw * t), P<void>(ws, L.dzgT + 2 * L.nhw * t), dbc, dbg,
                  first ? gmax : (const uint32_t*)nullptr, P<float>(ws, L.gbp) + (size_t)t * gb_stride * 3 * H,
-                 &gb_nwg, s);
+                 (first && c.sd) ? sb + (size_t)t * c.b * 512 : (const uint2*)nullptr, &gb_nwg, s);
     DISPATCH_VH(c, launch_prop_bwd, PREC, c, t, P<void>(ws, L.dXT), P<u16>(adj, AL.AbT), P<u16>(adj, AL.deg),
                 chan_lists(c, adj, AL), PL, pack,
                 dB, dh_out, P<void>(ws, L.dMT + (size_t)c.C * L.nhw * t),
                 use_bias ? P<float>(ws, L.dbp) + (size_t)t * c.b * c.C * c.H : nullptr,
-                last ? gmax : (const uint32_t*)nullptr, s);
+                last ? gmax : (const uint32_t*)nullptr, sb, s);
   }
   // all weight gradients in one grouped launch over every timestep (measured:
   // 20 % faster than one launch per timestep right after its producers, whose
   // operands would still sit in the Infinity Cache)
   if (int e = wgrad_impl<PREC>(c, adj, ws, 0, c.T, dW, dWg, dWc, s)) return e;
-  if (c.ed) {
-    Prof p(K_WGRAD, s);
-    hipLaunchKernelGGL(k_edge_mask_reduce, dim3(grid1d((long)c.C * H * H / 4)), dim3(256), 0, s,
-                       P<const float>(ws, L.G), dW, c.C, c.H, c.T, c.edrop);
-  }
   {
     Prof p(K_IO, s);
     if (!dense)
@@ -745,21 +781,24 @@ int backward_impl(const Cfg& c, const void* pack, const void* adj, void* ws, con
     sp.rows(P<const float>(ws, L.gbp), c.T, gb_nwg, gb_stride, 3 * H, dbg, dbc, 2 * H).ugmax = gmax;
     if (use_bias)
       sp.rows(P<const float>(ws, L.dbp), 1, c.T * c.b, c.T * c.b, (long)c.C * H, dbeta, dbeta, (long)c.C * H).ugmax = gmax;
-    sp.launch(s);
+    if (int e = sp.launch(s)) return e;
   }
 
   LAUNCHCHK();
   return GGNN_OK;
 }
 
-// Weight gradients of timesteps [t0, t0 + nt): out[m][n] += sum_{t,rows}
-// P_t[m][row] Q_t[n][row], one grouped launch (k_wgrad.h).
+// Weight gradients of timesteps [t0, t0 + nt): out[m][n] = sum_{t,rows}
+// P_t[m][row] Q_t[n][row], one grouped launch (k_wgrad.h).  The outputs are
+// STORED, not accumulated (k_wgrad_reduce writes each element once, already
+// unscaled): the one caller passes all timesteps at once (t0 = 0, nt = T).
 template <int PREC>
 int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* dW, float* dWg, float* dWc,
                hipStream_t s) {
   const WsL L = ws_layout(c, true);
   const long N = c.N, H = c.H;
   if (H < 128) return fail(GGNN_EUNSUP, "weight gradients need hidden >= 128");
+  if (t0 != 0 || nt != c.T) return fail(GGNN_EINVAL, "weight gradients: stored over all timesteps at once");
   WgArgs a;
   memset(&a, 0, sizeof(a));
   int np = 0, tiles = 0;
@@ -767,6 +806,8 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   // 256x256 tiles (k_wgrad256) at hidden = 256: every problem has M = 256
   const bool big = H == 256 && N % 128 == 0;
   const int TS = big ? 256 : 128;
+  const WgPlan wp = wg_plan(c);
+  int wgs = 0;
   auto add = [&](size_t Poff, long stepP, size_t Qoff, long stepQ, float* out, int ldO, int M, int Nn, int nb = 1,
                  long sQb = 0, long sOb = 0) {
     WgProb& p = a.p[np++];
@@ -778,6 +819,11 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
     p.sPb = 0; p.pdiv = 1; p.T = nt;
     p.tile_begin = tiles;
     tiles += nb * p.tiles_b;
+    p.nch = (int)wp.nchunks;
+    p.cpt = 0;
+    p.KCt = 0;
+    p.wg_begin = wgs;
+    wgs += nb * p.tiles_b * p.nch;
   };
   // d gates_kernel: rows [0,H) from X, rows [H,2H) from h ; columns dzg (2H)
   add(L.XT, sa, L.dzgT, 2 * sa, dWg, 2 * H, H, 2 * H);
@@ -785,28 +831,24 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   // d candidate_kernel: rows [0,H) from X, rows [H,2H) from r*h ; columns dzc (H)
   add(L.XT, sa, L.dzcT, sa, dWc, H, H, H);
   add(L.rhT, sa, L.dzcT, sa, dWc + H * H, H, H, H);
-  if (!c.ed) {
-    // d edge_weights[c] = sum_t h_t^T dM_{c,t}: one problem batched over the C channels
-    add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
-  } else {
-    // edge dropout: G[t][c] = h_t^T dM_{c,t} per timestep (batch index t*C + c),
-    // then dW[c] = sum_t mask_t/keep * G[t][c] (k_edge_mask_reduce)
-    add(L.hT, sa, L.dMT, c.C * sa, P<float>(ws, L.G) + (size_t)t0 * c.C * H * H, H, H, H, nt * c.C, sa,
-        (long)H * H);
+  // d edge_weights[c] = sum_t mask_t/keep (h_t^T dM_{c,t}): one problem batched
+  // over the C channels.  Under edge dropout its K chunks are timestep-aligned
+  // (wp.cpt chunks of wp.KCt rows per timestep): k_wgrad_reduce sums each
+  // timestep's chunks, applies that timestep's mask (Philox, as the pack drew
+  // it) and adds the timesteps in order
+  add(L.hT, sa, L.dMT, c.C * sa, dW, H, H, H, c.C, sa, (long)H * H);
+  if (c.ed) {
     WgProb& q = a.p[np - 1];
-    q.T = 1; q.sPb = sa; q.pdiv = c.C;
+    q.cpt = (int)wp.cpt;
+    q.KCt = (int)wp.KCt;
+    q.nch = (int)(nt * wp.cpt);
+    wgs = q.wg_begin + c.C * q.tiles_b * q.nch;
+    a.edrop = c.edrop;
   }
   constexpr int WP = WgradPrec<PREC>::value;
   a.nprob = np;
   a.H = (int)H;
-  // K chunks are sized by the tiles of T-summed problems: under edge dropout
-  // the dW problem runs per timestep (nt * C tiles of one timestep each), and
-  // counting those tiles halved the chunk count, doubling the slices of the
-  // GRU-gradient workgroups (all nt timesteps each), which then set the launch
-  // time (measured +0.27 ms per step at config 3 with keep 0.9)
-  const long tiles_eq = c.ed ? tiles - (long)(nt - 1) * c.C * a.p[np - 1].tiles_b : tiles;
-  const WgPlan wp = wg_plan(c);
-  if (wp.tiles_eq != tiles_eq || wp.tiles < tiles || wp.TS != TS)
+  if (wp.tiles != tiles || wp.wgs != wgs || wp.TS != TS)
     return fail(GGNN_EINVAL, "weight gradients: launch plan and workspace disagree");
   // deterministic reduction over the K chunks (k_wgrad_reduce): the partial
   // tiles live in the workspace
@@ -815,7 +857,7 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   if (big) {
     const long KC = wp.KC;
     if (N % KC || KC % 128) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
-    if (tiles_eq != 6 + c.C) return fail(GGNN_EINVAL, "k_wgrad256: unexpected problem set");
+    if (tiles != 6 + c.C) return fail(GGNN_EINVAL, "k_wgrad256: unexpected problem set");
     a.KC = (int)KC;
     a.nchunks = (int)(N / KC);
     if (wgrad_lists(c)) {
@@ -827,7 +869,7 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
       q.V32 = c.V / 32;
     }
     Prof p(K_WGRAD, s);
-    hipLaunchKernelGGL((k_wgrad256<WP>), dim3(tiles * a.nchunks), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_wgrad256<WP>), dim3(wgs), dim3(512), 0, s, a);
     hipLaunchKernelGGL(k_wgrad_reduce<256>, dim3(tiles * 64), dim3(256), 0, s, a);
     return GGNN_OK;
   }
@@ -835,11 +877,10 @@ int wgrad_impl(const Cfg& c, const void* adj, void* ws, int t0, int nt, float* d
   if (N % KC) return fail(GGNN_EUNSUP, "rows not divisible into weight-gradient chunks");
   a.KC = KC;
   a.nchunks = (int)(N / KC);
-  const int grid = tiles * a.nchunks;
   {
     Prof p(K_WGRAD, s);
-    if (KC % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, WP>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_wgrad<64, WP>), dim3(grid), dim3(256), 0, s, a);
+    if (KC % 64 != 0 || wp.KCt % 64 != 0) hipLaunchKernelGGL((k_wgrad<32, WP>), dim3(wgs), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad<64, WP>), dim3(wgs), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_wgrad_reduce<128>, dim3(tiles * 16), dim3(256), 0, s, a);
   }
   LAUNCHCHK();
@@ -926,6 +967,7 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
 extern "C" {
 #ifdef GGNN_TS
 int ggnn_dbg_ts(void* host) { return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ts), sizeof(g_ts)); }
+int ggnn_dbg_clk(void* host) { return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_clk), sizeof(g_clk)); }
 int ggnn_dbg_ts_clear(void) {
   static unsigned long long zero[sizeof(g_ts) / 8];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ts), zero, sizeof(g_ts));
@@ -1619,7 +1661,7 @@ static int heads_backward_impl(const ggnn_dims* d, const ggnn_output_head* heads
 #undef HDZ
     sp.add(dbp + L.off[i], 1, nbz, 0, Ot, o, o, 0, hd.d_bias, hd.d_bias, o);
   }
-  sp.launch(s);
+  if (int e = sp.launch(s)) return e;
   // dZ ~ 1/target_num per element: carried as S*dZ (S an exact power of two
   // <= target_num) so its f16 limbs stay normal; alpha = 1/S undoes it
   // (tn_dev: the GEMMs resolve S from the device value, GemmArgs::snum)

@@ -42,7 +42,16 @@ typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 __device__ unsigned long long g_ts[4][2048 * 8];
 #define TSMARK(k, i) do { if (threadIdx.x == 0) g_ts[k][blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TSVAL(k, i, v) do { if (threadIdx.x == 0) g_ts[k][blockIdx.x * 8 + (i)] = (unsigned long long)(v); } while (0)
+// in-kernel clock (MI355X_MICROARCH.md "DVFS give-back" item 6): shader-clock
+// ticks (s_memtime) and 100 MHz ticks (s_memrealtime) at a workgroup's start
+// and end; clock = d(memtime) / d(memrealtime) x 100 MHz.  Diagnostic build
+// only: the stamps go to g_clk, which nothing in the kernels reads.
+__device__ unsigned long long g_clk[4][2048 * 4];
+#define TSCLK(k, e) do { if (threadIdx.x == 0) { \
+    g_clk[k][blockIdx.x * 4 + 2 * (e)] = __builtin_amdgcn_s_memrealtime(); \
+    g_clk[k][blockIdx.x * 4 + 2 * (e) + 1] = __builtin_amdgcn_s_memtime(); } } while (0)
 #else
+#define TSCLK(k, e) do {} while (0)
 #define TSMARK(k, i) do {} while (0)
 #define TSVAL(k, i, v) do {} while (0)
 #endif

@@ -50,6 +50,12 @@ struct FusedFwdArgs {
   long sw, s4;
   int C, T, vsh;
   Drop sd;
+  // training under state dropout: the keep bits of every timestep's state mask
+  // (round 6), one uint2 per (timestep, graph, thread): bit (rt & 1) * 16 + r
+  // of word rt >> 1 = accumulator element r of row tile rt (the lane's column
+  // n = ns * 32 + l32).  k_prop_bwd and k_gru_bwd read them instead of drawing
+  // the same Philox blocks again.  Null: not written.
+  uint2* sbits;
 };
 
 // PREC: PREC_SPLIT (fp32-parity: f16 hi/lo limb images, 3 products) or a
@@ -58,6 +64,7 @@ struct FusedFwdArgs {
 template <int PREC>
 __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
   const Drop sd = drop_resolve(a.sd);  // (a device-resident key: loaded once)
+  TSCLK(2, 0);
   using namespace gru2;
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   // chunk -> ring slot / image limbs
@@ -367,6 +374,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
       const bool sav = a.u != nullptr;
       u16* hto = (a.hT && t + 1 < a.T) ? a.hT + (t + 1) * a.sw : nullptr;
       uint4 dw = make_uint4(0, 0, 0, 0);
+      uint32_t kb[2] = {0u, 0u};  // state keep bits (a.sbits)
       // every h_t load ahead of the first store: vmcnt retires in order, so a
       // load issued behind a row tile's stores would wait for them to drain
       float hp[RT][16];
@@ -389,6 +397,7 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
               dw = state_words(sd, g, rt * 32 + acc_row0(r) + 4 * hh, n, t);
             }
             x = drop_apply(sd, u4_get(dw, r & 3), x);
+            kb[rt >> 1] |= (uint32_t)(u4_get(dw, r & 3) < sd.thr) << ((rt & 1) * 16 + r);
           }
           hn[r] = x;
           bst(ho, x, vo, so);
@@ -422,7 +431,9 @@ __global__ void __launch_bounds__(512) k_fwd_fused(FusedFwdArgs a) {
                                  hn[4 * q + 2], hn[4 * q + 3]);
         }
       }
+      if (a.sbits && sd.thr) a.sbits[((long)t * gridDim.x + g) * NT + tid] = make_uint2(kb[0], kb[1]);
     }
     TSMARK(2, 6);
   }
+  TSCLK(2, 1);
 }

@@ -228,7 +228,7 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 //   [dX2 | dh2] = dzg @ Wg^T                       (K = 2H)
 //   out: dX^T = (dX1 + dX2)^T, dh + dh2 (fp32)
 // ===========================================================================
-// Weight limbs of k_gru_bwd's two products in the fp32-parity mode: WH = the
+// Weight limbs of k_gru_bwd's two products in the fp32-parity mode: the
 // hi limb of Wc^T / Wg^T only (2 MFMAs per k-step and output tile: dz_hi W_hi +
 // dz_lo W_hi; dz stays a hi/lo pair), instead of the hi/lo pair (3 MFMAs).
 // Half the weight fragments streamed from L2 per row tile (1.5 -> 0.75 MiB at
@@ -236,39 +236,31 @@ k_gru_fwd(const ActT<PREC>* __restrict__ Xa, const u16* __restrict__ hb16, const
 // backward_operand_policy, tests/test_precision_policies.py): max |err| /
 // max |ref| of the seven gradients 1.2e-4 -> 5.1e-4 on configs[2] data at
 // T = 5, against the 1e-3 fp32 bar.
-#ifndef GGNN_GB_WHI
-#define GGNN_GB_WHI 1
-#endif
-template <int PREC, bool WH, typename W>
-DEV void gb_mma(f32x16& a1, f32x16& a2, frag ah, frag al, const W& w) {
-  if constexpr (WH) {
-    mma_xb<PREC>(a1, ah, al, w.a);
-    mma_xb<PREC>(a2, ah, al, w.b);
-  } else {
-    mma<PREC>(a1, ah, al, w.a, w.b);
-    mma<PREC>(a2, ah, al, w.c, w.d);
-  }
+template <int PREC>
+DEV void gb_mma(f32x16& a1, f32x16& a2, frag ah, frag al, const F2& w) {
+  mma_xb<PREC>(a1, ah, al, w.a);
+  mma_xb<PREC>(a2, ah, al, w.b);
 }
 
-#ifndef GGNN_GB_RT1_OCC
-#define GGNN_GB_RT1_OCC 1
-#endif
 template <int H, int RT, int PREC>
-__global__ void __launch_bounds__(2 * H, RT == 1 ? 2 * GGNN_GB_RT1_OCC : 1)
+__global__ void __launch_bounds__(2 * H, RT == 1 ? 2 : 1)
 k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const float* __restrict__ rin,
           const float* __restrict__ uin, const float* __restrict__ cin, const u16* __restrict__ WcTp,
           const u16* __restrict__ WgTp, long wlo_c, long wlo_g, ActT<PREC>* __restrict__ dXT,
           float* __restrict__ dh_out, u16* __restrict__ dzcT, u16* __restrict__ dzgT,
           float* __restrict__ dbc, float* __restrict__ dbg, long N, const uint32_t* __restrict__ gmax,
-          float* __restrict__ bpart) {
+          float* __restrict__ bpart, const uint2* __restrict__ sbits, float sscale) {
   // bpart: this timestep's [workgroup][dbg (2H) | dbc (H)] rows of bias partials
-  // (summed in a fixed order by k_sum_rows: deterministic), or nullptr: atomics
-  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16, WH = SPLIT && GGNN_GB_WHI;
+  // (summed in a fixed order by k_sum_rows: deterministic), or nullptr: atomics.
+  // sbits (first backward step, dL/dh_T read in place under state dropout):
+  // the forward's keep bits of the last timestep's state mask (k_fwd_fused,
+  // 128-row graphs: word (graph, thread), bit (jt & 1) * 16 + r of word jt >> 1
+  // for row tile jt of the graph), applied to delta with scale sscale = 1/keep
+  constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   constexpr int NS = H / 32, KS = H / 16, R = 32 * RT, ZCH = 2 * H / 8;
-  // two 32-row workgroups per CU (GGNN_GB_RT1_OCC = 2) fit the 128-VGPR budget
-  // with a one-deep weight ring; the other workgroup hides its latency
-  constexpr int GBD = RT == 1 && GGNN_GB_RT1_OCC == 2 ? 1 : GB_DEPTH;
+  constexpr int GBD = GB_DEPTH;
   const float ds = gscale(gmax);  // gradient scale of dL/dh_T read in place (ggnn_common.h), else 1
+  TSCLK(1, 0);
   typedef Swz<ZCH> SZ;
   constexpr int NIMG = SPLIT ? 2 : 1;
   constexpr int IMG = R * 2 * H * 2;
@@ -291,6 +283,9 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   // delta, u, c, h; delta*u stays in registers for phase 2's dh
   float csum = 0.f, usum = 0.f;
   float du[RT][16];
+  uint2 kb = make_uint2(0u, 0u);
+  const int jt0 = (int)((row0 & 127) >> 5);  // first 32-row tile of this workgroup in its graph
+  if (sbits) kb = sbits[(row0 >> 7) * (2 * H) + tid];
   const rsrc_t pdo = mkrsrc(dh_out + tb0, tbytes);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -303,7 +298,12 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
         const int so = ro * H * 4;
-        const float d = bld_p<kGbAux>(pd, vo, so) * ds, u = uq[i], c = cq[i], h = bld_p<0>(ph, vo, so);
+        float d = bld_p<kGbAux>(pd, vo, so) * ds;
+        if (sbits) {
+          const int jt = jt0 + rt;
+          d = (((jt >> 1 ? kb.y : kb.x) >> ((jt & 1) * 16 + 4 * q + i)) & 1u) ? d * sscale : 0.0f;
+        }
+        const float u = uq[i], c = cq[i], h = bld_p<0>(ph, vo, so);
         dz[i] = d * (1.0f - u) * (1.0f - c * c);
         zu[i] = d * (h - c) * u * (1.0f - u);
         du[rt][4 * q + i] = d * u;
@@ -335,18 +335,13 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   f32x16 a1[RT], a2[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) { a1[rt] = splat(0.f); a2[rt] = splat(0.f); }
-  auto ld1 = [&](int ks) {
-    if constexpr (WH) return F2{frag_ld(WcTp, ns, ks, KS, lane), frag_ld(WcTp, NS + ns, ks, KS, lane)};
-    else
-      return F4{frag_ld(WcTp, ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, ns, ks, KS, lane) : frag{},
-                frag_ld(WcTp, NS + ns, ks, KS, lane), SPLIT ? frag_ld(WcTp + wlo_c, NS + ns, ks, KS, lane) : frag{}};
-  };
+  auto ld1 = [&](int ks) { return F2{frag_ld(WcTp, ns, ks, KS, lane), frag_ld(WcTp, NS + ns, ks, KS, lane)}; };
   b_pipeline<KS, GBD, GB_UNROLL>(ld1, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      gb_mma<PREC, WH>(a1[rt], a2[rt], ah, al, w);
+      gb_mma<PREC>(a1[rt], a2[rt], ah, al, w);
     }
   });
   __syncthreads();  // dzc reads done
@@ -386,19 +381,13 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   TSMARK(1, 3);
 
   // ---- product 2: [dX2 | dh2] = dzg @ Wg^T
-  auto ld2 = [&](int ks) {
-    if constexpr (WH) return F2{frag_ld(WgTp, ns, ks, 2 * KS, lane), frag_ld(WgTp, NS + ns, ks, 2 * KS, lane)};
-    else
-      return F4{frag_ld(WgTp, ns, ks, 2 * KS, lane), SPLIT ? frag_ld(WgTp + wlo_g, ns, ks, 2 * KS, lane) : frag{},
-                frag_ld(WgTp, NS + ns, ks, 2 * KS, lane),
-                SPLIT ? frag_ld(WgTp + wlo_g, NS + ns, ks, 2 * KS, lane) : frag{}};
-  };
+  auto ld2 = [&](int ks) { return F2{frag_ld(WgTp, ns, ks, 2 * KS, lane), frag_ld(WgTp, NS + ns, ks, 2 * KS, lane)}; };
   b_pipeline<2 * KS, GBD, GB_UNROLL>(ld2, [&](int ks, const auto& w) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int off = SZ::off(rt * 32 + l32, 2 * ks + hh);
       const frag ah = lds_frag(z_hi, off), al = SPLIT ? lds_frag(z_lo, off) : ah;
-      gb_mma<PREC, WH>(a1[rt], a2[rt], ah, al, w);
+      gb_mma<PREC>(a1[rt], a2[rt], ah, al, w);
     }
   });
   TSMARK(1, 4);
@@ -412,4 +401,5 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     for (int r = 0; r < 16; ++r) bst(pdo, a2[rt][r], vo, (rt * 32 + acc_row0(r)) * H * 4);
   }
   TSMARK(1, 5);
+  TSCLK(1, 1);
 }

@@ -145,9 +145,6 @@ k_prop_fwd(const ActT<PREC>* __restrict__ hs_in, const u16* __restrict__ Ab, con
 }
 
 // ===========================================================================
-#ifndef GGNN_PB_WHI
-#define GGNN_PB_WHI 1
-#endif
 // k_prop_bwd: backward of message + aggregation, per channel c
 //   dM_c^T[n][j] = sum_i dX^T[n][i] A_c[i][j]    (K = V; dX^T fragments stay in
 //                                                registers for all channels)
@@ -161,8 +158,12 @@ __global__ void __launch_bounds__(2 * H)
 k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, const u16* __restrict__ deg,
            const int* __restrict__ chl, int chs, const u16* __restrict__ WTp, long wlo, const float* __restrict__ dh_in, float* __restrict__ dh_out,
            u16* __restrict__ dMT, float* __restrict__ dbp, int C, long N, Drop dr, int tm,
-           const uint32_t* __restrict__ gmax, int zdm) {
+           const uint32_t* __restrict__ gmax, int zdm, const uint2* __restrict__ sbits) {
+  // sbits: the forward's state keep bits of timestep tm (k_fwd_fused,
+  // FusedFwdArgs::sbits; this kernel's lane / tile mapping is the same), or
+  // null: the mask's Philox blocks are drawn here
   dr = drop_resolve(dr);  // (a device-resident key: loaded once)
+  TSCLK(3, 0);
   constexpr bool SPLIT = Prec<PREC>::split, F16 = Prec<PREC>::f16;
   using Act = ActT<PREC>;
   constexpr int NS = H / 32, NT = 64 * NS, VT = V / 32, KV = V / 16, KS = H / 16;
@@ -258,24 +259,19 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    // (GGNN_PB_WHI, on: W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per
-    // tile instead of 3.  With k_gru_bwd's hi-only weights the oracle's
+    // (W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per tile instead of 3.  With k_gru_bwd's hi-only weights the oracle's
     // backward_operand_policy puts the gradients at <= 7.7e-4 of the 1e-3
     // bar (b = 256, T = 5, training dropout; profiles/r05_backward_policies.json)
     // and the GPU at 7.66e-4 (test_full_config3_all_gradients_vs_float64_oracle);
     // prop_bwd 0.642 -> 0.558 ms per config-3 step)
-    constexpr bool PWH = SPLIT && GGNN_PB_WHI;
-    auto ldb = [&](int ks) {
-      return F2{frag_ld(wt, ns, ks, KS, lane), (SPLIT && !PWH) ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
-    };
-    auto pb = [&](int ks, const F2& w) {
+    auto ldb = [&](int ks) { return frag_ld(wt, ns, ks, KS, lane); };
+    auto pb = [&](int ks, const frag& w) {
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt) {
         const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(m_hi, off);
         const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-        if constexpr (PWH) mma_xb<PREC>(adh[jt], ah, al, w.a);
-        else mma<PREC>(adh[jt], ah, al, w.a, SPLIT ? w.b : w.a);
+        mma_xb<PREC>(adh[jt], ah, al, w);
       }
     };
     b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)
@@ -312,6 +308,8 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   // dL/dh_t -> dL/dh'_{t-1} through the state dropout of timestep tm = t-1
   const bool drop = dr.thr != 0 && tm >= 0;
   const float osc = gunscale(gmax);  // last step writing dL/dh0 in place: undo the gradient scale, else 1
+  uint2 kb = make_uint2(0u, 0u);
+  if (drop && sbits) kb = sbits[((long)tm * gridDim.x + g) * NT + tid];
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt) {
     uint4 dw = make_uint4(0, 0, 0, 0);
@@ -319,8 +317,13 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     for (int r = 0; r < 16; ++r) {
       float x = adh[jt][r] * osc;
       if (drop) {
-        if ((r & 3) == 0) dw = state_words(dr, g, jt * 32 + acc_row0(r) + 4 * hh, n, tm);
-        x = drop_apply(dr, u4_get(dw, r & 3), x);
+        if (sbits) {
+          const uint32_t w = (VT == 4) ? ((jt >> 1) ? kb.y : kb.x) : kb.x;
+          x = ((w >> ((jt & 1) * 16 + r)) & 1u) ? x * dr.scale : 0.0f;
+        } else {
+          if ((r & 3) == 0) dw = state_words(dr, g, jt * 32 + acc_row0(r) + 4 * hh, n, tm);
+          x = drop_apply(dr, u4_get(dw, r & 3), x);
+        }
       }
       bst(rdo, x, vo, (jt * 32 + acc_row0(r)) * H * 4);
     }
@@ -343,4 +346,5 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         for (int q = tid; q < H; q += NT) dbp[((long)g * C + c) * H + q] = 0.f;
     }
   }
+  TSCLK(3, 1);
 }

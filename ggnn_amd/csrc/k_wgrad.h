@@ -1,5 +1,6 @@
 // k_wgrad.h -- weight gradients as one grouped split-K "NT" GEMM launch:
-//   out[m][n] += sum_{t < T} sum_{k in chunk} P_t[m][k] * Q_t[n][k]
+//   out[m][n] = sum_{t < T} sum_{chunks} sum_{k in chunk} P_t[m][k] * Q_t[n][k]
+// (stored once by k_wgrad_reduce, not accumulated onto out)
 // P_t / Q_t are the transposed activations saved per timestep ([M][K] and
 // [N][K], K = the b*V node rows), each a stack of [H][K] arrays in the
 // K-blocked wg_off layout (ggnn_common.h).  Problems (reference autodiff,
@@ -14,6 +15,11 @@
 // gradient unscale, WgArgs::gmax) -- the same bits whatever order the
 // workgroups ran in (with part == nullptr: one fp32 atomicAdd per
 // output element and chunk, order-dependent).
+// Edge dropout (round 6): the dW problem's chunks are timestep-aligned
+// (WgProb::cpt chunks of KCt rows inside ONE timestep each, chunk k at
+// timestep k / cpt), and k_wgrad_reduce forms
+//   dW_c[i][j] = sum_t mask_t(c,i,j)/keep * (sum of timestep t's chunks)
+// with the pack's Philox draws (edge_words: counter (i>>2, j, c, t)).
 #pragma once
 #include "ggnn_common.h"
 
@@ -32,6 +38,10 @@ struct WgProb {
   // gls: [count, graph, ...]; a graph is V32 slices of 32 rows.  nullptr: all rows.
   const int* gl;
   int gls, glmod, V32;
+  // workgroups of this problem: tiles x nch chunks, from workgroup wg_begin
+  // (its partial tiles at part + (wg_begin + tile_local * nch + chunk) * TS^2).
+  // cpt > 0: timestep-aligned chunks (cpt per timestep, KCt rows each)
+  int nch, cpt, KCt, wg_begin;
 };
 #define WG_LIST_MAX 256  // graphs of one K chunk held in registers (4 VGPRs)
 #define WG_MAXP 8
@@ -39,9 +49,34 @@ struct WgArgs {
   WgProb p[WG_MAXP];
   int nprob, nchunks, KC;
   int H;  // rows of one operand array (wg_off layout); ldP / ldQ hold its N
-  float* part;  // [tiles][nchunks][TS * TS] partial tiles (deterministic reduction), or nullptr: atomics
+  float* part;  // partial tiles (deterministic reduction, one per workgroup), or nullptr: atomics
   const uint32_t* gmax;  // if set: k_wgrad_reduce stores the sums times the gradient unscale (gunscale)
+  Drop edrop;            // edge dropout of the timestep-aligned problem (thr 0: off)
 };
+
+// (problem, tile of the launch, chunk) of workgroup `wg`
+struct WgWork {
+  int pi, tile, chunk;
+};
+DEV WgWork wg_work(const WgArgs& args, int wg) {
+  int pi = 0;
+  while (pi + 1 < args.nprob && args.p[pi + 1].wg_begin <= wg) ++pi;
+  const WgProb& pr = args.p[pi];
+  const int local = wg - pr.wg_begin;
+  return WgWork{pi, pr.tile_begin + local / pr.nch, local % pr.nch};
+}
+// K range of a workgroup: rows [kbase, kbase + kits * BK) of timesteps
+// [t0, t0 + nt) (T-summed problems: chunk * KC, all T; timestep-aligned:
+// timestep chunk / cpt, rows (chunk % cpt) * KCt)
+struct WgK {
+  long kbase;
+  int kits, t0, nt;
+};
+template <int BK>
+DEV WgK wg_k(const WgArgs& args, const WgProb& pr, int chunk) {
+  if (pr.cpt) return WgK{(long)(chunk % pr.cpt) * pr.KCt, pr.KCt / BK, chunk / pr.cpt, 1};
+  return WgK{(long)chunk * args.KC, args.KC / BK, 0, pr.T};
+}
 
 // (problem, batch index, tile origin) of tile `tile` (TS x TS tiles)
 struct WgTile {
@@ -82,17 +117,37 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(WgArgs args) {
   constexpr int BPT = TS * TS / 1024;  // blocks per tile
   const int tile = blockIdx.x / BPT;
   const int f = (blockIdx.x % BPT) * 256 + threadIdx.x;
-  const float* src = args.part + (long)tile * args.nchunks * (TS * TS) + f * 4;
-  float4 s = *(const float4*)src;
-  for (int c = 1; c < args.nchunks; ++c) {
-    const float4 x = *(const float4*)(src + (long)c * (TS * TS));
-    s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
-  }
   const WgTile wt = wg_tile<TS>(args, tile);
   const WgProb& pr = args.p[wt.pi];
   const int lane = f & 63, q = (f >> 6) & 3, j = (f >> 8) % NJ, i = (f >> 8) / NJ % NI, wv = (f >> 8) / (NJ * NI);
   const int m = wt.m0 + (wv / WN) * WMR + i * 32 + acc_row(4 * q, lane >> 5);
   const int nn = wt.n0 + (wv % WN) * WNC + j * 32 + (lane & 31);
+  const float* src = args.part + (long)(pr.wg_begin + (tile - pr.tile_begin) * pr.nch) * (TS * TS) + f * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pr.cpt && args.edrop.thr) {
+    // edge dropout: timestep t's chunks summed in order, times mask_t / keep
+    // (rows m..m+3 = one Philox block's 4 words: m is a multiple of 4), then
+    // the timesteps in order
+    const Drop dr = drop_resolve(args.edrop);
+    for (int t = 0; t < pr.T; ++t) {
+      float4 st = *(const float4*)(src + (long)t * pr.cpt * (TS * TS));
+      for (int c = 1; c < pr.cpt; ++c) {
+        const float4 x = *(const float4*)(src + (long)(t * pr.cpt + c) * (TS * TS));
+        st.x += x.x; st.y += x.y; st.z += x.z; st.w += x.w;
+      }
+      const uint4 w = edge_words(dr, wt.bi, m, nn, t);
+      s.x += drop_apply(dr, w.x, st.x);
+      s.y += drop_apply(dr, w.y, st.y);
+      s.z += drop_apply(dr, w.z, st.z);
+      s.w += drop_apply(dr, w.w, st.w);
+    }
+  } else {
+    s = *(const float4*)src;
+    for (int c = 1; c < pr.nch; ++c) {
+      const float4 x = *(const float4*)(src + (long)c * (TS * TS));
+      s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+    }
+  }
   float* o = pr.out + (long)wt.bi * pr.sOb + (long)m * pr.ldO + nn;
   const float us = gunscale(args.gmax);
   o[0] = s.x * us;
@@ -111,11 +166,9 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
   constexpr int BUF = 2 * NIMG * TB;         // P and Q images of one stage
   constexpr int PT = 128 * CH / 256;         // 8-element chunks per thread per operand
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  const int tile = blockIdx.x / args.nchunks, chunk = blockIdx.x % args.nchunks;
-  int pi = 0;
-  while (pi + 1 < args.nprob && args.p[pi + 1].tile_begin <= tile) ++pi;
-  const WgProb pr = args.p[pi];
-  const int lt0 = tile - pr.tile_begin;
+  const WgWork wk = wg_work(args, blockIdx.x);
+  const WgProb pr = args.p[wk.pi];
+  const int lt0 = wk.tile - pr.tile_begin;
   const int bi = lt0 / pr.tiles_b, lt = lt0 % pr.tiles_b;
   const int m0 = (lt / pr.tiles_n) * 128, n0 = (lt % pr.tiles_n) * 128;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
@@ -123,10 +176,11 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs args) {
   constexpr int RPB = 256 / (BK * 2);        // tile rows per 256-B LDS bank row
   auto soff = [&](int row, int ch) { return row * BK * 2 + ((ch ^ ((row / RPB) & (CH - 1))) << 4); };
 
-  const int kits = args.KC / BK, nit = kits * pr.T, H = args.H;
-  const long kbase = (long)chunk * args.KC;
-  const Act* Pb = (const Act*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
-  const Act* Qb = (const Act*)pr.Q + (long)bi * pr.sQb;
+  const WgK K = wg_k<BK>(args, pr, wk.chunk);
+  const int kits = K.kits, nit = kits * K.nt, H = args.H;
+  const long kbase = K.kbase;
+  const Act* Pb = (const Act*)pr.P + (long)(bi / pr.pdiv) * pr.sPb + (long)K.t0 * pr.stepP;
+  const Act* Qb = (const Act*)pr.Q + (long)bi * pr.sQb + (long)K.t0 * pr.stepQ;
   float* const outp = pr.out + (long)bi * pr.sOb;
   // staging registers: one 8-element chunk = 16 B (bf16) or 32 B (fp32)
   typedef typename std::conditional<SPLIT, float4, uint4>::type V4;
@@ -252,11 +306,10 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   __shared__ __attribute__((aligned(16))) char sq0[TB], sq1[TB], sq2[TB], sq3[TB];  // Q images
   auto pslot = [&](int u) -> char* { return u == 0 ? sp0 : u == 1 ? sp1 : u == 2 ? sp2 : sp3; };
   auto qslot = [&](int u) -> char* { return u == 0 ? sq0 : u == 1 ? sq1 : u == 2 ? sq2 : sq3; };
-  const int tile = blockIdx.x / args.nchunks, chunk = blockIdx.x % args.nchunks;
-  int pi = 0;
-  while (pi + 1 < args.nprob && args.p[pi + 1].tile_begin <= tile) ++pi;
-  const WgProb pr = args.p[pi];
-  const int lt0 = tile - pr.tile_begin;
+  TSCLK(0, 0);
+  const WgWork wk = wg_work(args, blockIdx.x);
+  const WgProb pr = args.p[wk.pi];
+  const int lt0 = wk.tile - pr.tile_begin;
   const int bi = lt0 / pr.tiles_b, lt = lt0 % pr.tiles_b;
   const int m0 = (lt / pr.tiles_n) * 256, n0 = (lt % pr.tiles_n) * 256;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
@@ -264,20 +317,23 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   // image: row r = 64 B, chunk slot pc holds logical chunk pc ^ ((r >> 2) & 3)
   auto soff = [](int row, int ch) { return row * BK * 2 + ((ch ^ ((row >> 2) & 3)) << 4); };
 
-  const u16* Pb = (const u16*)pr.P + (long)(bi / pr.pdiv) * pr.sPb;
-  const u16* Qb = (const u16*)pr.Q + (long)bi * pr.sQb;
+  const WgK K = wg_k<BK>(args, pr, wk.chunk);
+  const u16* Pb = (const u16*)pr.P + (long)(bi / pr.pdiv) * pr.sPb + (long)K.t0 * pr.stepP;
+  const u16* Qb = (const u16*)pr.Q + (long)bi * pr.sQb + (long)K.t0 * pr.stepQ;
   float* const outp = pr.out + (long)bi * pr.sOb;
-  // K slices: the chunk's KC rows (kits slices) x T timesteps, or, with a graph
+  // K slices: the chunk's rows (kits slices) x its timesteps, or, with a graph
   // list, the chunk's share of the listed graphs' slices (any count: nit may
   // be 0 -- nothing to add -- and need not be a multiple of NBUF)
-  int kits = args.KC / BK;
-  long kbase = (long)chunk * args.KC;
+  int kits = K.kits;
+  long kbase = K.kbase;
   int glr[4] = {0, 0, 0, 0};  // the chunk's graphs, lane-distributed (read back by readlane)
   bool listed = false;        // K walks the list (else the contiguous rows from kbase)
   if (pr.gl) {
     const int* list = pr.gl + (long)(bi % pr.glmod) * pr.gls;
-    const int cnt = list[0], per = (cnt + args.nchunks - 1) / args.nchunks;
-    const int gb = min(cnt, chunk * per), ge = min(cnt, gb + per);
+    // a timestep-aligned problem splits the list over its cpt chunks of a timestep
+    const int nsplit = pr.cpt ? pr.cpt : args.nchunks, ci = pr.cpt ? wk.chunk % pr.cpt : wk.chunk;
+    const int cnt = list[0], per = (cnt + nsplit - 1) / nsplit;
+    const int gb = min(cnt, ci * per), ge = min(cnt, gb + per);
     kits = (ge - gb) * pr.V32;
     if (ge > gb) {
       const int g0 = list[1 + gb], g1 = list[ge];
@@ -290,7 +346,7 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
       }
     }
   }
-  const int nit = kits * pr.T;
+  const int nit = kits * K.nt;
   if (nit == 0 && !args.part) return;  // (partials: a zero tile still has to be stored)
   // row of slice `it`'s first K element: graph glr[i] (i = slice / V32) row (slice % V32) * 32
   auto krow = [&](int sl) -> long {
@@ -359,6 +415,7 @@ __global__ void __launch_bounds__(512) k_wgrad256(WgArgs args) {
   for (int u = 0; u < nit - nfull; ++u) slice(nfull + u, u);
   if (args.part) {
     wg_store_part<4, 2>(args.part + (long)blockIdx.x * (256 * 256), acc, wv, lane);
+    TSCLK(0, 1);
     return;
   }
 #pragma unroll

@@ -451,24 +451,33 @@ class DenseGGNNChemModel(BtbBatching):
                           torch.full((cap,), -1, dtype=torch.int32, device=self.device))
         return self._rows
 
+    @staticmethod
+    def _sparse_call(fl, reducer) -> bool:
+        """Whether THIS step reduces the word table as IndexedSlices: the
+        buffer has the sparse region and the reducer can gather (a
+        dist.Reducer).  Without a reducer (a local step) or with a plain
+        callable, the word table's gradient is written densely into its view
+        of the buffer (and a plain callable all-reduces the whole buffer)."""
+        return bool(fl.sparse) and reducer is not None and hasattr(reducer, "gather")
+
     def _reduce(self, fl, reducer, started=None) -> None:
         """The data-parallel reduction of one step's flat buffer: the dense
         part as (heads + losses) and the rest -- the first bucket possibly
         started already (``started``: its handle) -- and, with the sparse
-        reduction on, the word table as the union of every rank's lookups:
-        the ranks' (rows, ids) all-gathered, accumulated in fixed point
-        (exact, so the same bits on every rank)."""
-        if fl.sparse and not hasattr(reducer, "gather"):
-            raise TypeError("the sparse word-table reduction needs a dist.Reducer (all_reduce_sum()), "
-                            "or params['sparse_embedding_reduce'] = False")
+        reduction on (_sparse_call), the word table as the union of every
+        rank's lookups: the ranks' (rows, ids) all-gathered, accumulated in
+        fixed point (exact, so the same bits on every rank).  A plain
+        callable reducer sums the whole buffer in one blocking call (the word
+        table dense, as the step wrote it)."""
+        sparse = self._sparse_call(fl, reducer)
         if not hasattr(reducer, "start"):          # a plain callable: one blocking all-reduce
-            reducer(fl.dense)
+            reducer(fl.flat)
         else:
             b0, b1 = fl.buckets
             h0 = started if started is not None else reducer.start(b0)
             reducer(b1)
             reducer.wait(h0)
-        if fl.sparse:
+        if sparse:
             rows, ids = self._lookup_rows()
             g_rows, g_ids = reducer.gather(rows), reducer.gather(ids)
             if self._front_end is None:
@@ -525,7 +534,7 @@ class DenseGGNNChemModel(BtbBatching):
     def _empty_train_step(self, all_reduce, grad_scale):
         fl = self.train_buffer()
         fl.zero_()
-        if fl.sparse:                 # no lookups of this rank in the union
+        if self._sparse_call(fl, all_reduce):   # no lookups of this rank in the union
             self._lookup_rows()[0].zero_()
             self._lookup_rows()[1].fill_(-1)
         if all_reduce is not None:
@@ -575,7 +584,9 @@ class DenseGGNNChemModel(BtbBatching):
         keeps = (float(ph.get("emb_dropout_keep_prob", 1.0)),) + self._path_keeps() + (self._out_keep(),)
         adam = training and all_reduce is None
         # (grad_scale is baked into the captured Adam launch: part of the key)
-        key = (bool(training), adam, b, v, wi.shape[-1], keeps, task_id, float(grad_scale) if adam else 1.0)
+        # (the word table's layout, dense or IndexedSlices, is captured too)
+        sparse = bool(training) and self._sparse_call(self.train_buffer(), all_reduce)
+        key = (bool(training), adam, b, v, wi.shape[-1], keeps, task_id, float(grad_scale) if adam else 1.0, sparse)
         if training:
             fl = self.train_buffer()
             params = self.trainable_variables()
@@ -612,7 +623,9 @@ class DenseGGNNChemModel(BtbBatching):
 
         def body():
             if training:
-                probs = self._forward_backward(fl, params, None, task_id, sf)
+                # (the reducer only decides the word table's layout here: the
+                # collectives run after the replay, RCCL is not captured)
+                probs = self._forward_backward(fl, params, None, task_id, sf, reducer=None if adam else all_reduce)
                 if adam:
                     self._apply_gradients(fl, params, grad_scale, step_dev=inp.step)
                 loss = fl.loss.sum()
@@ -754,6 +767,15 @@ class DenseGGNNChemModel(BtbBatching):
         self._check_front_end_width()
         if sf is None:
             sf = self._eager_step_feed(task_id, target_count)
+        # the word table's reduction is decided per call: sparse
+        # only when a gathering reducer follows; checked before any work or
+        # collective is issued, so a rank cannot leave a step its peers wait in
+        sparse = self._sparse_call(fl, reducer)
+        if sparse:
+            cap = self._lookup_rows()[0].shape[0]
+            if sf.b * sf.v > cap:
+                raise ValueError("batch of %d x %d nodes exceeds the word lookup-row capacity %d (batch_size x "
+                                 "bucket_max_nodes)" % (sf.b, sf.v, cap))
         h = self.params["hidden_size"]
         gv = {id(p): g for p, g in zip(params, fl.grads)}
         # front-end (chem_tensorflow_dense.py:264-306)
@@ -804,7 +826,6 @@ class DenseGGNNChemModel(BtbBatching):
         eng.backward(dhT, eg)
         # the tables' gradients + IndexedSlices norms (h0 feeds the path and the heads)
         word = self.weights["word_embeddings"]
-        sparse = bool(fl.sparse)
         dts = [None if (sparse and t is word) else gv[id(t)] for t in tables]
         self._front_end.backward(segs, sf.wi, eg["h0"], keep_e, sf.seeds[0], dh0_add=dh0_heads,
                                  dtables=dts, sq_out=fl.sq, seed_device=sf.seed_device)

@@ -72,6 +72,25 @@ def main():
                                           gi.view(-1), sq)
     res["union_recomputed_equal"] = bool(torch.equal(again, word))
     res["lookups"] = int((gi >= 0).sum())
+    # the word table's layout is decided per call.  A sparse-layout
+    # model stepped WITHOUT a reducer (a local step) writes its word gradient
+    # densely, exactly as a dense-layout model does; with a plain callable
+    # reducer it sums the whole buffer and equals the dense-layout Reducer step
+    ml_d, ml_s = model(False), model(True)
+    ml_d.train_step(dict(feed), all_reduce=None, target_count=count)
+    ml_s.train_step(dict(feed), all_reduce=None, target_count=count)
+    torch.cuda.synchronize()
+    ld, ls = ml_d.train_buffer(), ml_s.train_buffer()
+    res["local_step_word_grad_equal"] = bool(torch.equal(ld.grads[wi], ls.grads[wi])) and \
+        float(ls.grads[wi].abs().max()) > 0
+    res["local_step_params_equal"] = all(torch.equal(a.detach(), b.detach()) for a, b in
+                                         zip(ml_d.trainable_variables(), ml_s.trainable_variables()))
+    mp = model(True)
+    mp.train_step(dict(feed), all_reduce=lambda t: tdist.all_reduce(t), target_count=count)
+    torch.cuda.synchronize()
+    fp = mp.train_buffer()
+    res["plain_callable_equals_dense"] = all(torch.equal(a, b) for a, b in zip(fd.grads, fp.grads)) and \
+        bool(torch.equal(fd.sq, fp.sq)) and bool(torch.equal(fd.loss, fp.loss))
     if rank == 0:
         with open(out, "w") as f:
             json.dump(res, f)

@@ -328,6 +328,11 @@ def test_bench_starts_its_own_ranks_without_torchrun():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 512, res
     assert res["all_reduce"]["backend"] == "gloo" and res["launcher"] == "bench.py"
+    # the strong-scaling split and the all-reduce's cost keys
+    assert res["strong_scaling"]["per_rank_batch"] == 128 and res["strong_scaling"]["global_batch"] == 256, res
+    ar = res["all_reduce"]
+    assert ar["bytes"] == 3681280 and ar["isolated_ms_per_call"] > 0 and ar["bus_bandwidth_gbs"] > 0, ar
+    assert ar["isolated_ms_per_call_min_rank"] <= ar["isolated_ms_per_call"], ar
 
 
 def test_bench_refuses_a_world_size_that_disagrees_with_gpus():

@@ -171,6 +171,16 @@ def test_bench_self_started_two_ranks():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 512 and res["config"]["parallelism"] == "dp2"
     assert res["all_reduce"]["backend"] == "gloo" and res["value"] > 0
+    # the strong leg (256 graphs split 128 per rank), the
+    # all-reduce's event time and bus bandwidth, the min / max rank step
+    st = res["strong_scaling"]
+    assert st["per_rank_batch"] == 128 and st["global_batch"] == 256 and st["value"] > 0, st
+    assert st["ms_per_step_min_rank"] <= st["ms_per_step"], st
+    ar = res["all_reduce"]
+    assert ar["in_step_ms"] > 0 and ar["isolated_ms_per_call"] > 0 and ar["bus_bandwidth_gbs"] > 0, ar
+    assert ar["in_step_ms_min_rank"] <= ar["in_step_ms"], ar
+    rs = res["rank_step_ms"]
+    assert 0 < rs["min"] <= rs["max"] and abs(rs["max"] - res["ms_per_step"]) < 1e-9, rs
 
 
 def test_two_rank_captured_step_returns_the_union_loss(tmp_path):
@@ -209,6 +219,10 @@ def test_sparse_word_reduction_matches_the_flat_one(tmp_path):
     assert r["sparse_layout"] and r["dense_grads_equal"] and r["loss_equal"] and r["params_equal_but_word"], r
     assert r["word_grad_rel"] <= 1e-6 and r["word_sq_rel"] <= 1e-5, r
     assert r["ranks_agree"] and r["union_recomputed_equal"] and r["lookups"] > 0, r
+    # no reducer -> the word gradient is written densely (not stale);
+    # a plain callable reducer sums the whole buffer like the dense layout
+    assert r["local_step_word_grad_equal"] and r["local_step_params_equal"], r
+    assert r["plain_callable_equals_dense"], r
 
 
 def test_rccl_one_rank_group_runs_the_training_collectives(tmp_path):
@@ -255,3 +269,6 @@ def test_bench_one_rank_rccl_rehearsal():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 1 and res["value"] > 0
     assert res["all_reduce"]["backend"] == "nccl" and res["all_reduce"]["bytes_per_step"] > 0
+    # the one-rank group still runs (and times) the collective; strong = weak at N = 1
+    assert res["all_reduce"]["in_step_ms"] > 0 and res["all_reduce"]["isolated_ms_per_call"] > 0
+    assert res["strong_scaling"]["per_rank_batch"] == 256 and res["strong_scaling"]["ms_per_step"] == res["ms_per_step"]

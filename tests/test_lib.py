@@ -61,7 +61,8 @@ def test_null_pointers_are_rejected_without_gpu(lib):
 
 def test_dropout_dims_validation_and_sizes(lib):
     """Keep probabilities must lie in (0, 1]; edge dropout holds one masked
-    weight copy per timestep in the pack and a per-timestep dW scratch."""
+    weight copy per timestep in the pack, and its dW problem's timestep-aligned
+    K chunks (round 6) take their own split-K partial tiles."""
     import ctypes
     from ggnn_amd import _lib
     for ek, sk in ((0.0, 1.0), (1.0, 0.0), (1.5, 1.0), (1.0, -0.1), (float("nan"), 1.0)):
@@ -76,9 +77,13 @@ def test_dropout_dims_validation_and_sizes(lib):
     # and the general path's keep bits of every timestep (round 5: [T][C][h][h/32] words)
     assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4) + 5 * 8 * 256 * 8 * 4
     assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
-    # + the per-timestep dW scratch G [T][C][h][h], and the (T-1) C extra
-    # per-timestep dW tiles' split-K partials (16 K chunks at b = 256, v = 128:
-    # k_wgrad_reduce's deterministic reduction)
+    # the dW problem's K chunks under edge dropout: 4 per timestep (T = 5: 20)
+    # instead of 16 spanning every timestep -- 4 more 256 x 256 partial tiles per
+    # channel for k_wgrad_reduce's deterministic reduction (no per-timestep dW
+    # scratch since round 6: the reduce applies each timestep's mask itself)
+    # (the forward's state keep bits, round 6, are laid out with or without
+    # state dropout: a workspace sized for keep 1 serves keep < 1 too)
     assert (_lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True)
-            == 5 * 8 * 256 * 256 * 4 + 4 * 8 * 16 * 256 * 256 * 4)
+            == 8 * (5 * 4 - 16) * 256 * 256 * 4)
+    assert _lib.workspace_bytes(d3, True) == _lib.workspace_bytes(d1, True)
     assert _lib.workspace_bytes(d2, False) == _lib.workspace_bytes(d1, False)
