@@ -274,6 +274,40 @@ def precision_error(dev, precision, host, T):
     return out
 
 
+def strong_split_side(dev, A, h0, dhT, w_d, v, h, C, T, precision, steps=20):
+    """Side measurement (rank 0 at N = 1): the step on 256/N graphs -- the
+    per-rank work of the strong-scaling leg at N = 2, 4, 8 -- on this one GPU,
+    without the all-reduce: the strong-scaling curve's compute part.  One
+    workgroup per graph in the fused forward and k_prop_bwd means a batch
+    below 256 graphs leaves CUs idle, so this is where strong scaling stops."""
+    import torch
+    from ggnn_amd.dist import FlatGradients
+    from ggnn_amd.engine import PropagationEngine
+    res = {}
+    for n in (2, 4, 8):
+        bs = A.shape[0] // n
+        eng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=precision)
+        grads = FlatGradients(h, C, True, device=dev)
+        gv = dict(grads.views)
+        gv["h0"] = torch.empty((bs, v, h), dtype=torch.float32, device=dev)
+        out = torch.empty((bs, v, h), dtype=torch.float32, device=dev)
+        A_s, h0_s, d_s = (torch.from_numpy(np.ascontiguousarray(x[:bs])).to(dev) for x in (A, h0, dhT))
+
+        def step():
+            pack = eng.pack_weights(w_d, T=T)
+            eng.set_adjacency(A_s)
+            eng.forward(h0_s, pack, T, training=True, out=out)
+            eng.backward(d_s, gv)
+
+        ms = _timed_events(step, steps)
+        res["n%d" % n] = {"per_rank_batch": bs, "ms_per_step": ms, "graphs_per_s_per_gpu": bs / (ms * 1e-3)}
+        del eng, grads, gv, out, A_s, h0_s, d_s
+        torch.cuda.empty_cache()
+    res["note"] = ("fwd+bwd of 256/N graphs on one GPU (no optimizer, no all-reduce): the per-rank compute of the "
+                   "strong-scaling leg; strong-scaling speedup <= 256-graph step / this step")
+    return res
+
+
 def gru_inference_leg(eng, h0_d, w_d, A_d, b, v, h, C, T, precision, steps=10):
     """The unfused forward in inference mode (training=False: no saves for the
     backward), k_gru_fwd timed per launch with HIP events.  SURVEY §8(d)'s GRU
@@ -1020,6 +1054,8 @@ def main():
     fp16 = (precision_side(dev, "fp16", A_d, h0_d, w_d, dhT, b, v, h, C, T, host=host_slice)
             if rank == 0 and not args.no_side and args.precision != "fp16" else None)
     real = real_density_side(dev) if rank == 0 and not args.no_side else None
+    strong1 = (strong_split_side(dev, A, h0, dhT.cpu().numpy(), w_d, v, h, C, T, args.precision)
+               if rank == 0 and world == 1 and not args.no_side else None)
 
     if rank == 0:
         fpg = flops_per_graph(v, h, C, T)["total"]
@@ -1083,6 +1119,7 @@ def main():
             "bf16_mode": bf16,
             "fp16_mode": fp16,
             "real_density_c92": real,
+            "strong_split_one_gpu": strong1,
             "end_to_end_run_epoch": e2e,
         }
         if world == 1 and not args.no_cpu_baseline:

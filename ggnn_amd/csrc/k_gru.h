@@ -21,10 +21,7 @@ constexpr int kGbAux = kNT;
 // full unrolling, which spills at H = 256)
 constexpr int GF_UNROLL = 2, GB_UNROLL = 2;
 // k_gru_bwd's weight-fragment ring depth (k-steps in flight)
-#ifndef GGNN_GB_DEPTH
-#define GGNN_GB_DEPTH 2
-#endif
-constexpr int GB_DEPTH = GGNN_GB_DEPTH;
+constexpr int GB_DEPTH = 2;
 
 // gru_bwd elementwise phases: loads of GB_GROUP row quads (x 4 arrays) in flight
 // between scheduling barriers (measured: 4 > 2 > 1; VGPRs stay within budget)

@@ -242,6 +242,9 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
       // dbeta_c[n] = sum_i dX[i][n] deg_c[i] as one more MFMA product: B[i][*] =
       // deg_c[i] (exact integers), every output column holds the sum.  Per-graph
       // partials [b][C][H] (no atomics); reduced over graphs after the last step.
+      // (Round 6 tried the column sums of the dM^T accumulators instead -- a lane
+      // butterfly, 16 fewer MFMAs per channel and wave -- and the extra live
+      // registers spilled 29-69 VGPRs at 256: not kept.)
       const uint4* dg = (const uint4*)(deg + ((long)g * C + c) * V);  // wave-uniform: scalar loads
       f32x16 db = splat(0.f);
 #pragma unroll
@@ -259,19 +262,22 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    // (W_c^T's hi limb only, dM hi/lo x W hi: 2 MFMAs per tile instead of 3.  With k_gru_bwd's hi-only weights the oracle's
-    // backward_operand_policy puts the gradients at <= 7.7e-4 of the 1e-3
-    // bar (b = 256, T = 5, training dropout; profiles/r05_backward_policies.json)
-    // and the GPU at 7.66e-4 (test_full_config3_all_gradients_vs_float64_oracle);
-    // prop_bwd 0.642 -> 0.558 ms per config-3 step)
-    auto ldb = [&](int ks) { return frag_ld(wt, ns, ks, KS, lane); };
-    auto pb = [&](int ks, const frag& w) {
+    // W_c^T as an f16 hi/lo limb pair (3 MFMAs per tile in the split mode).
+    // Round 5 took the hi limb only here AND in k_gru_bwd; round 6 measured
+    // that on more inputs (oracle backward_operand_policy, b = 8, T = 5..8,
+    // eight seeds): up to 1.07e-3 of the 1e-3 bar, while hi-only weights in
+    // k_gru_bwd alone stay <= 7.6e-4 (tests/test_precision_policies.py,
+    // test_gpu_parity.py::test_backward_hi_weight_limbs_long_unroll)
+    auto ldb = [&](int ks) {
+      return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
+    };
+    auto pb = [&](int ks, const F2& w) {
 #pragma unroll
       for (int jt = 0; jt < VT; ++jt) {
         const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
         const frag ah = lds_frag(m_hi, off);
         const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-        mma_xb<PREC>(adh[jt], ah, al, w);
+        mma<PREC>(adh[jt], ah, al, w.a, w.b);
       }
     };
     b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)

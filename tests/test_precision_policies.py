@@ -94,10 +94,26 @@ def test_backward_policy_exact_equals_oracle_backward(bwd_case):
 
 def test_backward_weight_hi_limbs_hold_the_fp32_bar(bwd_case):
     shipped_r4 = _bwd_err(bwd_case, "f16x2", "f16x2", "f16x2", "f16")
-    gru_only = _bwd_err(bwd_case, "f16x2", "f16", "f16x2", "f16")       # k_gru_bwd: Wc^T / Wg^T hi limbs
-    shipped_r5 = _bwd_err(bwd_case, "f16x2", "f16", "f16", "f16")       # + k_prop_bwd's W_c^T (GGNN_PB_WHI)
+    shipped_r6 = _bwd_err(bwd_case, "f16x2", "f16", "f16x2", "f16")     # k_gru_bwd: Wc^T / Wg^T hi limbs
+    r5 = _bwd_err(bwd_case, "f16x2", "f16", "f16", "f16")               # + k_prop_bwd's W_c^T hi limb (round 5)
     assert shipped_r4 <= 2.5e-4, shipped_r4
-    assert gru_only < shipped_r5, (gru_only, shipped_r5)
-    # the shipped policy: measured 6.4e-4 (b = 4); 7.7e-4 at b = 256 with training
-    # dropout, the worst case of the table (GPU: 7.66e-4)
-    assert shipped_r4 < shipped_r5 <= 9e-4, (shipped_r4, shipped_r5)
+    assert shipped_r4 < shipped_r6 < r5, (shipped_r4, shipped_r6, r5)
+    assert shipped_r6 <= 8e-4, shipped_r6
+
+
+@pytest.mark.parametrize("seed,T", [(31, 5), (31, 8), (5, 5)])
+def test_backward_policy_margin_over_seeds_and_unrolls(seed, T):
+    """the round-5 backward (hi weight limbs in k_gru_bwd AND
+    k_prop_bwd) was pinned at one seed and T = 5.  Over other inputs and the
+    longer unroll it reaches the 1e-3 bar (seed 31: 1.07e-3 at T = 5, 1.10e-3 at
+    T = 8; seed 5: 9.9e-4), so round 6 gives k_prop_bwd its W_c^T lo limb back:
+    hi limbs in k_gru_bwd only, <= 7.6e-4 on every case measured (b = 8,
+    T = 5..8, eight seeds)."""
+    A, h0 = O.synthetic_batch(8, V, H, C, seed=seed)
+    w = {k: x.astype(np.float64) for k, x in O.synthetic_weights(H, C, seed=seed).items()}
+    A, h0 = A.astype(np.float64), h0.astype(np.float64)
+    _, caches = O.forward(A, h0, w, T)
+    dhT = np.random.default_rng(15 if seed == 31 else seed + 100).standard_normal(h0.shape)
+    ref = O.backward(A, dhT, caches, w)
+    case = (A, dhT, caches, w, ref)
+    assert _bwd_err(case, "f16x2", "f16", "f16x2", "f16") <= 8e-4

@@ -18,5 +18,8 @@ cp gpurun_out/${TAG}_pmc/pmc_traffic.json profiles/pmc_traffic.json
 PMC_RUN=$TAG bash tools/pmc_profile.sh gpurun_out/${TAG}_pmcbf16 --steps 2 --warmup 1 --no-cpu-baseline --no-side \
   --precision bf16 --pmc-unfused-leg > gpurun_out/${TAG}_pmcbf16.log 2>&1
 cp gpurun_out/${TAG}_pmcbf16/pmc_traffic.json profiles/pmc_traffic_bf16.json
+# inference-only forwards (no saves): the GRU's bytes against SURVEY §8d's 12 v h
+bash tools/pmc_profile_infer.sh gpurun_out/${TAG}_pmcinfer bf16 > gpurun_out/${TAG}_pmcinfer.log 2>&1
+cp gpurun_out/${TAG}_pmcinfer/pmc_traffic.json profiles/pmc_traffic_bf16_infer.json
 timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_bench.log 2>&1
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1

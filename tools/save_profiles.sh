@@ -13,5 +13,9 @@ if [ -d gpurun_out/${TAG}_pmcbf16 ]; then
   cp gpurun_out/${TAG}_pmcbf16.log profiles/${TAG}_bf16_pmc_table.txt
   cp gpurun_out/${TAG}_pmcbf16/pmc_traffic.json profiles/pmc_traffic_bf16.json
 fi
+if [ -d gpurun_out/${TAG}_pmcinfer ]; then
+  cp gpurun_out/${TAG}_pmcinfer/summary.json profiles/${TAG}_bf16_infer_pmc_summary.json
+  cp gpurun_out/${TAG}_pmcinfer/pmc_traffic.json profiles/pmc_traffic_bf16_infer.json
+fi
 [ -f gpurun_out/${TAG}_gputests.log ] && cp gpurun_out/${TAG}_gputests.log profiles/${TAG}_gputests.log
 true
