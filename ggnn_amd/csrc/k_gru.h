@@ -25,7 +25,7 @@ constexpr int GB_DEPTH = 2;
 
 // gru_bwd elementwise phases: loads of GB_GROUP row quads (x 4 arrays) in flight
 // between scheduling barriers (measured: 4 > 2 > 1; VGPRs stay within budget)
-constexpr int GB_GROUP = 4, GB_GROUP2 = 4;
+constexpr int GB_GROUP = 4;
 
 // ===========================================================================
 // k_gru_fwd
@@ -277,9 +277,11 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
   TSMARK(1, 0);
 
   // ---- phase 1: dzc, and the u half of dzg (needs no product): one read of
-  // delta, u, c, h; delta*u stays in registers for phase 2's dh
+  // delta, u, c, h and r; delta*u and r stay in registers for phase 2 (round
+  // 6: phase 2 loaded r from HBM after product 1, a lockstep memory phase;
+  // now it re-reads only h, which phase 1 left in L2)
   float csum = 0.f, usum = 0.f;
-  float du[RT][16];
+  float du[RT][16], rk[RT][16];
   uint2 kb = make_uint2(0u, 0u);
   const int jt0 = (int)((row0 & 127) >> 5);  // first 32-row tile of this workgroup in its graph
   if (sbits) kb = sbits[(row0 >> 7) * (2 * H) + tid];
@@ -290,7 +292,9 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
     for (int q = 0; q < 4; ++q) {
       float dz[4], zu[4];
       const float4 u4 = bld4_p<kGbAux>(pu, qm_vo(hh, n, H), qm_so(rt, q, H)), c4 = bld4_p<kGbAux>(pc, qm_vo(hh, n, H), qm_so(rt, q, H));
+      const float4 r4 = bld4_p<kGbAux>(pr, qm_vo(hh, n, H), qm_so(rt, q, H));
       const float uq[4] = {u4.x, u4.y, u4.z, u4.w}, cq[4] = {c4.x, c4.y, c4.z, c4.w};
+      rk[rt][4 * q] = r4.x; rk[rt][4 * q + 1] = r4.y; rk[rt][4 * q + 2] = r4.z; rk[rt][4 * q + 3] = r4.w;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ro = rt * 32 + acc_row0(4 * q + i);
@@ -351,14 +355,11 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float zr[4];
-      const float4 r4 = bld4_p<kGbAux>(pr, qm_vo(hh, n, H), qm_so(rt, q, H));
-      const float rq[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * q + i;
         const int ro = rt * 32 + acc_row0(r);
-        const int so = ro * H * 4;
-        const float h = bld_p<0>(ph, vo, so), rr = rq[i];
+        const float h = bld_p<0>(ph, vo, ro * H * 4), rr = rk[rt][r];
         const float drh = a2[rt][r];
         a2[rt][r] = du[rt][r] + drh * rr;
         zr[i] = drh * h * rr * (1.0f - rr);
@@ -366,7 +367,6 @@ k_gru_bwd(const float* __restrict__ delta, const float* __restrict__ hf, const f
         img_put<PREC, ZCH>(z_hi, z_lo, ro + 4 * hh, n, zr[i]);
       }
       st_col4w<PREC>(dzgT + twg + rt * 32 * H + 8 * q, zr[0], zr[1], zr[2], zr[3]);
-      if ((q & (GB_GROUP2 - 1)) == GB_GROUP2 - 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
   rsum += __shfl_xor(rsum, 32);
