@@ -940,11 +940,19 @@ def main():
     with timer:
         dt_instr = timed(step, args.steps, 1.0, ar_events)
     # the same step with the training-feed dropout (keep 0.9 for both), reported beside
-    dt_drop = float("nan")
+    # Timed in alternating blocks of K/2 steps (off, on, off, on) so that the
+    # two are compared on the same clock state: a leg timed minutes after the
+    # headline region sees another DVFS state of the chip
+    dt_drop = dt_drop_off = float("nan")
     if not args.no_dropout_leg:
         for _ in range(args.warmup):
             step(args.dropout_keep)
-        dt_drop = timed(step, args.steps, args.dropout_keep)
+        half = max(args.steps // 2, 1)
+        on, off = [], []
+        for _ in range(2):
+            off.append(timed(step, half))
+            on.append(timed(step, half, args.dropout_keep))
+        dt_drop, dt_drop_off = float(np.mean(on)), float(np.mean(off))
     # strong scaling: the global batch of 256 graphs split
     # 256/N per rank, timed exactly like the weak leg.  At N = 1 it IS the weak leg.
     bs = strong_batch(world)
@@ -972,8 +980,9 @@ def main():
         torch.cuda.synchronize()
         ar_in_step = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ar_events]))
     ar_iso = all_reduce_costs(grads.flat, reps=max(args.steps, 10))
-    (dt, dt_drop, dt_strong, dt_instr, ar_max), (dt_min, dt_drop_min, dt_strong_min, _, ar_min) = rank_spread(
-        [dt, dt_drop, dt_strong, dt_instr, ar_in_step if ar_in_step is not None else float("nan")], dev)
+    (dt, dt_drop, dt_strong, dt_instr, ar_max, dt_drop_off), (dt_min, dt_drop_min, dt_strong_min, _, ar_min, _) = \
+        rank_spread([dt, dt_drop, dt_strong, dt_instr, ar_in_step if ar_in_step is not None else float("nan"),
+                     dt_drop_off], dev)
 
     if args.pmc_unfused_leg:
         ueng = PropagationEngine(h, C, use_edge_bias=True, device=dev, precision=args.precision,
@@ -1113,8 +1122,12 @@ def main():
             "dropout_on": None if args.no_dropout_leg else {
                            "edge_keep": args.dropout_keep, "state_keep": args.dropout_keep,
                            "value": world * b / dt_drop, "ms_per_step": dt_drop * 1e3,
-                           "note": "same step with the reference's training-feed dropout (:860-861); "
-                                   "value above is dropout off (keep 1, the parity setting)"},
+                           "dropout_off_adjacent_ms_per_step": dt_drop_off * 1e3,
+                           "ratio_to_adjacent_off": dt_drop / dt_drop_off,
+                           "note": "same step with the reference's training-feed dropout (:860-861), timed in "
+                                   "alternating K/2-step blocks with the dropout-off step (off, on, off, on): "
+                                   "ms_per_step = the on blocks, dropout_off_adjacent_ms_per_step = the off "
+                                   "blocks; value above is dropout off (keep 1, the parity setting)"},
             "callers": callers,
             "bf16_mode": bf16,
             "fp16_mode": fp16,

@@ -206,6 +206,11 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   if (nc > 0) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(0) * V * V, tid);
   const rsrc_t rdh = mkrsrc(dh_in + rowg * H, V * H * 4);
   const int vo = (4 * hh * H + n) * 4;
+  // the forward's state keep bits of timestep tm, loaded here so the
+  // epilogue's stores do not wait for them
+  const bool drop = dr.thr != 0 && tm >= 0;
+  uint2 kb = make_uint2(0u, 0u);
+  if (drop && sbits) kb = sbits[((long)tm * gridDim.x + g) * NT + tid];
   f32x16 adh[VT];
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt)
@@ -312,10 +317,7 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
   }
   const rsrc_t rdo = mkrsrc(dh_out + rowg * H, V * H * 4);
   // dL/dh_t -> dL/dh'_{t-1} through the state dropout of timestep tm = t-1
-  const bool drop = dr.thr != 0 && tm >= 0;
   const float osc = gunscale(gmax);  // last step writing dL/dh0 in place: undo the gradient scale, else 1
-  uint2 kb = make_uint2(0u, 0u);
-  if (drop && sbits) kb = sbits[((long)tm * gridDim.x + g) * NT + tid];
 #pragma unroll
   for (int jt = 0; jt < VT; ++jt) {
     uint4 dw = make_uint4(0, 0, 0, 0);

@@ -139,7 +139,10 @@ const char* ggnn_last_error(void);
 int ggnn_check_dims(const ggnn_dims* d);
 
 /* Bytes of the per-batch workspace (activations saved for backward when
- * training != 0), of one staged adjacency batch and of one weight pack. */
+ * training != 0), of one staged adjacency batch and of one weight pack.
+ * The workspace size depends on b, v, h, C, T, flags, training and on whether
+ * edge dropout is on (edge_keep < 1), not on state_keep or the seed: one
+ * workspace serves every state-dropout setting of its shape. */
 int ggnn_workspace_bytes(const ggnn_dims* d, int training, size_t* bytes);
 int ggnn_adjacency_bytes(const ggnn_dims* d, size_t* bytes);
 int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes);

@@ -7,7 +7,8 @@ step time and the HIP-event kernel breakdown.
     GGNN_LIB=other.so python tools/ab_step.py ...   (a library build A/B: two runs)
 
 Variants: skip (channel skipping, the default engine), dense
-(skip_empty_channels=False), keepXX (training dropout at keep 0.XX).
+(skip_empty_channels=False), keepXX (training dropout at keep 0.XX), ekXX /
+stXX (edge-weight / state dropout alone at keep 0.XX).
 """
 import argparse
 import json
@@ -68,11 +69,16 @@ def main():
 
     def make(variant):
         keep = 1.0
+        ekeep = skeep = None     # edge / state keep when they differ (variants ekXX, stXX)
         kw = {}
         if variant == "dense":
             kw["skip_empty_channels"] = False
         elif variant.startswith("keep"):
             keep = float("0." + variant[4:])
+        elif variant.startswith("ek"):
+            ekeep, skeep = float("0." + variant[2:]), 1.0
+        elif variant.startswith("st"):
+            ekeep, skeep = 1.0, float("0." + variant[2:])
         eng = PropagationEngine(h, C, device=dev, **kw)
         if args.reference:
             eng.set_adjacency_edges(graphs, v, C // 2)      # once, as bench.py's real-density lines
@@ -84,10 +90,12 @@ def main():
 
         def step():
             n[0] += 1
-            pack = eng.pack_weights(w_d, T=T, edge_keep=keep, seed=n[0])
+            ek = keep if ekeep is None else ekeep
+            sk = keep if skeep is None else skeep
+            pack = eng.pack_weights(w_d, T=T, edge_keep=ek, seed=n[0])
             if not args.reference:
                 eng.set_adjacency(A_d)
-            eng.forward(h0_d, pack, T, training=True, out=out, state_keep=keep)
+            eng.forward(h0_d, pack, T, training=True, out=out, state_keep=sk)
             eng.backward(dhT, gv)
             opt.step([grads.views[k] for k in GRAD_ORDER])
         return step
