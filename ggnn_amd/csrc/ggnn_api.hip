@@ -264,7 +264,13 @@ WgPlan wg_plan(const Cfg& c) {
   if (c.ed) {
     // about as many chunks as the T-summed problems have (the same work per
     // workgroup): the smallest power of two >= nchunks / T whose chunk is a
-    // whole number of 32-row slices, else one chunk per timestep
+    // whole number of 32-row slices, else one chunk per timestep.  (At
+    // config 3 the 20 chunks per channel tile put the C channels' workgroups
+    // of one chunk -- which read the same h_t^T rows -- on different XCDs:
+    // +170 MB of HBM reads, L2 hit rate 0.50 -> 0.44, PMC
+    // profiles/r06j_pmc_dropout_*.txt; 40 chunks, a multiple of the 8 XCDs,
+    // took two rounds of workgroups and measured slower: wgrad 0.333 -> 0.350
+    // ms per step, profiles/r06k_ab_cfg3_dw_chunks.log)
     long cpt = 1;
     while (cpt * c.T < w.nchunks && N % (cpt * 2 * 32) == 0) cpt *= 2;
     w.cpt = cpt;

@@ -319,17 +319,18 @@ def _bench(args, env_extra=None, timeout=240):
                           timeout=timeout, env=env)
 
 
-def test_bench_starts_its_own_ranks_without_torchrun():
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_starts_its_own_ranks_without_torchrun(n):
     import json
-    r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--launch-only"])
+    r = _bench(["--gpus", str(n), "--dist-backend", "gloo", "--launch-only"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 512, res
+    assert res["n_gpus"] == n and res["config"]["global_batch"] == 256 * n, res
     assert res["all_reduce"]["backend"] == "gloo" and res["launcher"] == "bench.py"
     # the strong-scaling split and the all-reduce's cost keys
-    assert res["strong_scaling"]["per_rank_batch"] == 128 and res["strong_scaling"]["global_batch"] == 256, res
+    assert res["strong_scaling"]["per_rank_batch"] == 256 // n and res["strong_scaling"]["global_batch"] == 256, res
     ar = res["all_reduce"]
     assert ar["bytes"] == 3681280 and ar["isolated_ms_per_call"] > 0 and ar["bus_bandwidth_gbs"] > 0, ar
     assert ar["isolated_ms_per_call_min_rank"] <= ar["isolated_ms_per_call"], ar

@@ -78,9 +78,9 @@ def test_dropout_dims_validation_and_sizes(lib):
     assert p2 - p1 == 4 * 2 * (2 * 8 * 256 * 256 * 2) + 4 * (8 * 256 * 256 * 4) + 5 * 8 * 256 * 8 * 4
     assert _lib.weight_pack_bytes(d3) == p1                   # state dropout needs no extra pack
     # the dW problem's K chunks under edge dropout: 4 per timestep (T = 5: 20)
-    # instead of 16 spanning every timestep -- 4 more 256 x 256 partial tiles per
-    # channel for k_wgrad_reduce's deterministic reduction (no per-timestep dW
-    # scratch since round 6: the reduce applies each timestep's mask itself)
+    # instead of 16 spanning every timestep -- 4 more 256 x 256 partial tiles
+    # per channel for k_wgrad_reduce's deterministic reduction (no per-timestep
+    # dW scratch since round 6: the reduce applies each timestep's mask itself)
     # (the forward's state keep bits, round 6, are laid out with or without
     # state dropout: a workspace sized for keep 1 serves keep < 1 too)
     assert (_lib.workspace_bytes(d2, True) - _lib.workspace_bytes(d1, True)

@@ -10,6 +10,7 @@ for v in skip ek90; do
   i=0
   for grp in "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" "FETCH_SIZE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
     i=$((i+1))
+    mkdir -p "$OUT/$v"
     timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/$v/pass$i" -o p -- python3 tools/ab_step.py --variants $v --rounds 1 --steps 10 > "$OUT/$v/pass$i.log" 2>&1
   done
   python3 tools/pmc_summary.py "$OUT/$v" > "$OUT/$v.txt"
