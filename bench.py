@@ -1084,7 +1084,9 @@ def main():
             "precision_note": {"fp32": "fp32-class: every non-exact MFMA operand of the forward and of the "
                                        "dh/dX chain as an f16 hi/lo limb pair (3 products), fp32 accumulation, "
                                        "except k_gru_bwd's Wc^T / Wg^T (the hi limb only: dz hi/lo x W hi, 2 "
-                                       "products); the weight-gradient GEMMs (k_wgrad256) take SINGLE f16 "
+                                       "products) and k_prop_bwd's dM W_c^T (hi x hi on f16 MFMAs, both limb "
+                                       "corrections on the block-scaled fp8 MFMA: e5m2 dM, e4m3 W_c^T); the "
+                                       "weight-gradient GEMMs (k_wgrad256) take SINGLE f16 "
                                        "operands, on a power-of-two-scaled gradient; parity <= 1e-3 vs the fp32 "
                                        "reference (tests/test_gpu_parity.py, incl. loss-scale gradients; the "
                                        "backward's limb policy: tests/test_precision_policies.py)",

@@ -505,6 +505,10 @@ bool wgrad_lists(const Cfg& c) {
   return (c.b + per_t - 1) / per_t <= WG_LIST_MAX && c.V % 32 == 0;
 }
 
+// k_prop_bwd's dh += dM W_c^T with its limb corrections on the fp8 MFMA
+// (ggnn_common.h mfma_f8corr): the fp32-parity mode, hidden a multiple of 32
+bool prop_f8(const Cfg& c) { return c.prec == PREC_SPLIT && c.H % 32 == 0; }
+
 template <int V, int H, int PREC>
 void launch_prop_bwd(const Cfg& c, int t, const void* dXT, const u16* AbT, const u16* deg, ChanL chl,
                      const PackL& PL, const void* pk, const float* dh_in, float* dh_out, void* dMT, float* dbp,
@@ -914,12 +918,12 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
     nb = 0;
   };
   auto job = [&](const float* S, int ldS, long sS, int K, int N, int trans, void* out, long sO, long lo, int batch,
-                 int t, int drop) {
+                 int t, int drop, int f8 = 0) {
     if (a.count == PACK_MAXJ) flush();  // (long T under edge dropout)
     PackJob& J = a.j[a.count];
     J.S = S; J.out = (u16*)out; J.sS = sS; J.sO = sO; J.lo_off = lo;
     J.total = (long)batch * (N / 32) * (K / 16) * 64;
-    J.ldS = ldS; J.K = K; J.N = N; J.trans = trans; J.t = t; J.drop = drop; J.copy = 0;
+    J.ldS = ldS; J.K = K; J.N = N; J.trans = trans; J.t = t; J.drop = drop; J.copy = 0; J.f8 = f8;
     a.blk_begin[a.count++] = nb;
     nb += (int)((J.total + 255) / 256);
   };
@@ -942,12 +946,15 @@ int pack_impl(const Cfg& c, void* pack, const unsigned char* chocc, const float*
   if (L.fast) {
     for (int t = 0; t < (c.ed ? c.T : 1); ++t) {  // one masked copy per timestep under edge dropout
       job(W, H, (long)H * H, H, H, 0, P<u16>(pack, L.wf(t)), (long)H * H, L.loW, c.C, t, c.ed);  // MT: Bmat = W_c
-      job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed);  // dh: Bmat = W_c^T
+      // dh: Bmat = W_c^T; fp32-parity mode: fp8 correction fragments (k_prop_bwd, mfma_f8corr)
+      job(W, H, (long)H * H, H, H, 1, P<u16>(pack, L.wt(t)), (long)H * H, L.loW, c.C, t, c.ed, prop_f8(c));
     }
     job(Wg, 2 * H, 0, 2 * H, 2 * H, 0, P<u16>(pack, L.Wg), 0, L.loWg, 1, 0, 0);
-    job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0);
+    // k_gru_bwd's W^T packs: fp32-parity mode: fp8 lo fragments (gb_f8_product)
+    const int gf8 = c.prec == PREC_SPLIT ? 2 : 0;
+    job(Wg, 2 * H, 0, 2 * H, 2 * H, 1, P<u16>(pack, L.WgT), 0, L.loWg, 1, 0, 0, gf8);
     job(Wc, H, 0, 2 * H, H, 0, P<u16>(pack, L.Wc), 0, L.loWc, 1, 0, 0);   // Bmat = Wc   [2H][H]
-    job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0);  // Bmat = Wc^T [H][2H]
+    job(Wc, H, 0, H, 2 * H, 1, P<u16>(pack, L.WcT), 0, L.loWc, 1, 0, 0, gf8);  // Bmat = Wc^T [H][2H]
   }
   copy((c.flags & GGNN_USE_EDGE_BIAS) ? beta : nullptr, P<float>(pack, L.beta), (long)c.C * H);
   copy(bg, P<float>(pack, L.bg), 2L * H);

@@ -193,6 +193,43 @@ DEV void mma_xb(f32x16& acc, frag ah, frag al, frag b) {
   acc = mfma<Prec<PREC>::f16>(ah, b, acc);
 }
 
+// ---- limb corrections on the block-scaled fp8 MFMA (fp32-parity mode, k_prop_bwd's
+// dh += dM W_c^T).  The split product a.b = a_hi b_hi + a_hi b_lo + a_lo b_hi takes
+// its main term on v_mfma_f32_32x32x16_f16 (2 per 32 k) and BOTH correction terms
+// of 32 k's on one v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64, twice the cycles of
+// one 16-bit 32x32x16 form): 4 instead of 6 cycle units per 32 k.  Operand layout
+// (measured, tools/mx_hybrid_probe.hip, profiles/r06n_mx_layout.json): lane l holds
+// 32 bytes; A byte j of lane l meets B byte j of lane l' iff l >> 5 == l' >> 5
+// (row = A lane & 31, column = B lane & 31); bytes 0-15 of both lane halves take
+// the scale of lane (l & 31), bytes 16-31 that of lane (l & 31) + 32.  Here:
+//   A lane half 0: e5m2(a)            A lane half 1: e5m2(a_lo 2^F8_M)
+//   B lane half 0: e4m3(b_lo 2^(F8_Q + F8_M))   B lane half 1: e4m3(b_hi 2^F8_Q)
+// each byte j = k offset j inside the 32-k block; both halves carry 2^(F8_Q+F8_M),
+// which B's E8M0 scale (127 - F8_Q - F8_M) removes.  The activation side is
+// e5m2 (range 2^-16 .. 57344, no per-block scale needed); the weight side e4m3
+// with a fixed 2^F8_Q: |W| up to 448 / 2^F8_Q = 3.5 is represented, larger
+// weights saturate (k_pack_multi clamps), which costs only correction-term
+// accuracy.  Error budget (oracle emulation, tools/precision_policies.py
+// --hybrid): the seven gradients' max |err| / max |ref| unchanged (5.3-6.6e-4
+// against 5.3-6.6e-4 for the 3-product form, b = 8, T = 5 and 8).
+constexpr int F8_Q = 7, F8_M = 11;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// 4 floats -> 4 packed bytes (byte i = value i), OCP e5m2 / e4m3, RNE
+DEV uint32_t pk4_bf8(float a, float b, float c, float d) {
+  uint32_t w = (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(c, d, (int)w, true);
+}
+DEV uint32_t pk4_fp8(float a, float b, float c, float d) {
+  uint32_t w = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, (int)w, true);
+}
+// D += (A8 . B8) 2^-(F8_Q + F8_M): A e5m2, B e4m3, one 32x32x64 MFMA
+DEV f32x16 mfma_f8corr(uint4 a0, uint4 a1, uint4 b0, uint4 b1, f32x16 c) {
+  const i32x8 fa = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+  const i32x8 fb = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb, c, 1, 0, 0, 127, 0, 127 - F8_Q - F8_M);
+}
+
 // XOR swizzle of 16-byte chunks inside rows of NCH chunks so that the 32
 // distinct rows of one MFMA operand read land on distinct LDS bank slots.
 template <int NCH>

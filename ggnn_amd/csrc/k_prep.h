@@ -499,6 +499,13 @@ struct PackJob {
   uint32_t* bits;
   long sS, sO, lo_off, total;  // total: fragment-lanes (pack) or elements (copy)
   int ldS, K, N, trans, t, drop, copy;
+  // f8 = 1: the lo part holds the fp8 correction fragments of mfma_f8corr (ggnn_common.h)
+  // instead of f16 lo limbs: [strip][32-k block][64 lanes][32 bytes], lane half 0
+  // e4m3(b_lo 2^(F8_Q+F8_M)), half 1 e4m3(b_hi 2^F8_Q) (the same bytes as the limbs;
+  // k_prop_bwd).  f8 = 2: [strip][64-k block][64 lanes][32 bytes] of e4m3(b_lo
+  // 2^(F8_Q+F8_M)), byte j of lane half hh = k 64 kb + 32 hh + j (half the bytes;
+  // k_gru_bwd)
+  int f8;
 };
 struct PackJobs {
   PackJob j[PACK_MAXJ];
@@ -617,6 +624,39 @@ __global__ void __launch_bounds__(256) k_pack_multi(PackJobs a) {
     }
   }
   *(uint4*)(ob + (size_t)r * 8) = pk8<F16>(x);
+  if (J.f8 == 2) {
+    // k_gru_bwd's fp8 lo fragments: e4m3(b_lo 2^(F8_Q+F8_M)); this thread's 8 k's
+    // (k0 .. k0 + 7) are bytes (k0 & 31) .. + 7 of lane (col) + 32 ((k0 & 63) >> 5)
+    // of 64-k block k0 >> 6
+    float lo[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float h = (float)(_Float16)x[e];
+      lo[e] = fminf(fmaxf((x[e] - h) * (float)(1 << (F8_Q + F8_M)), -448.0f), 448.0f);
+    }
+    char* f8 = (char*)(ob + J.lo_off) +
+               ((size_t)(strip * (nks / 4) + (k0 >> 6)) * 64 + (lane & 31) + 32 * ((k0 & 63) >> 5)) * 32 + (k0 & 31);
+    *(uint2*)f8 = make_uint2(pk4_fp8(lo[0], lo[1], lo[2], lo[3]), pk4_fp8(lo[4], lo[5], lo[6], lo[7]));
+    return;
+  }
+  if (J.f8) {
+    // this thread's 8 k's (k0 .. k0 + 7 = 32 kb + 16 (ks & 1) + 8 (lane >> 5) + e)
+    // go to bytes 16 (ks & 1) + 8 (lane >> 5) + e of lane (col) [lo] and lane
+    // (col) + 32 [hi] of block kb's fragment
+    float lo[8], hi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float h = (float)(_Float16)x[e];
+      const float cl = 448.0f;
+      lo[e] = fminf(fmaxf((x[e] - h) * (float)(1 << (F8_Q + F8_M)), -cl), cl);
+      hi[e] = fminf(fmaxf(h * (float)(1 << F8_Q), -cl), cl);
+    }
+    const int kb = ks >> 1, byte = 16 * (ks & 1) + 8 * (lane >> 5);
+    char* f8 = (char*)(ob + J.lo_off) + ((size_t)(strip * (nks / 2) + kb) * 64 + (lane & 31)) * 32 + byte;
+    *(uint2*)f8 = make_uint2(pk4_fp8(lo[0], lo[1], lo[2], lo[3]), pk4_fp8(lo[4], lo[5], lo[6], lo[7]));
+    *(uint2*)(f8 + 32 * 32) = make_uint2(pk4_fp8(hi[0], hi[1], hi[2], hi[3]), pk4_fp8(hi[4], hi[5], hi[6], hi[7]));
+    return;
+  }
   *(uint4*)(ob + J.lo_off + (size_t)r * 8) = pk8_lo<F16>(x);
 }
 

@@ -237,9 +237,17 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
         const uint32_t p0 = pk<F16>(am[4 * q], am[4 * q + 1]), p1 = pk<F16>(am[4 * q + 2], am[4 * q + 3]);
         const int mo = kimg<V>(j, n0 >> 3) + (n0 & 7) * 2;  // chunk-major dM image
         *(uint2*)(m_hi + mo) = make_uint2(p0, p1);
-        if constexpr (SPLIT)
-          *(uint2*)(m_lo + mo) =
-              make_uint2(pk_lo<true>(am[4 * q], am[4 * q + 1]), pk_lo<true>(am[4 * q + 2], am[4 * q + 3]));
+        if constexpr (SPLIT) {
+          // fp8 correction image (mfma_f8corr's A operand): per row j and 32-column
+          // block ns, 4 chunks [e5m2(dM) n 0-15 | n 16-31 | e5m2(dM_lo 2^F8_M) n 0-15 | n 16-31]
+          const int o = 8 * q + 4 * hh;  // this quad's offset inside the wave's 32 columns
+          float lo[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lo[i] = lo_part<true>(am[4 * q + i]) * (float)(1 << F8_M);
+          const int m8 = kimg<V>(j, 4 * ns + (o >> 4)) + (o & 15);
+          *(uint32_t*)(m_lo + m8) = pk4_bf8(am[4 * q], am[4 * q + 1], am[4 * q + 2], am[4 * q + 3]);
+          *(uint32_t*)(m_lo + m8 + 2 * V * 16) = pk4_bf8(lo[0], lo[1], lo[2], lo[3]);
+        }
         dq[jt][q] = quad_transpose4(p0, p1, l32 & 3);
       }
     }
@@ -267,25 +275,56 @@ k_prop_bwd(const ActT<PREC>* __restrict__ dXT, const u16* __restrict__ AbT, cons
     if (ci + 1 < nc) glds_tile<ACH, V, NT, kPropAAux>(abuf, ag + (long)chan(ci + 1) * V * V, tid);
     // ---- phase b: dh[j][k] += sum_n dM_c[j][n] W_c^T[n][k]
     const u16* wt = WTp + (size_t)c * H * H;
-    // W_c^T as an f16 hi/lo limb pair (3 MFMAs per tile in the split mode).
-    // Round 5 took the hi limb only here AND in k_gru_bwd; round 6 measured
-    // that on more inputs (oracle backward_operand_policy, b = 8, T = 5..8,
-    // eight seeds): up to 1.07e-3 of the 1e-3 bar, while hi-only weights in
-    // k_gru_bwd alone stay <= 7.6e-4 (tests/test_precision_policies.py,
-    // test_gpu_parity.py::test_backward_hi_weight_limbs_long_unroll)
-    auto ldb = [&](int ks) {
-      return F2{frag_ld(wt, ns, ks, KS, lane), SPLIT ? frag_ld(wt + wlo, ns, ks, KS, lane) : frag{}};
-    };
-    auto pb = [&](int ks, const F2& w) {
+    // Split mode: dM and W_c^T both as hi + lo (round 5's hi-only W_c^T reached
+    // 1.07e-3 of the 1e-3 bar, tests/test_precision_policies.py); since round 6
+    // the two correction terms run on the fp8 MFMA (4 instead of 6 cycle units
+    // per 32 k; their error is 2^-15 of the product against 2^-12 for a dropped
+    // limb: the gradients' error does not move, tools/precision_policies.py --hybrid)
+    if constexpr (SPLIT) {
+      // per 32-column block kb of dM: the hi product on two 32x32x16 f16 MFMAs,
+      // both limb corrections on one fp8 32x32x64 (mfma_f8corr; W_c^T's
+      // correction fragments sit where its f16 lo limbs would, k_pack_multi f8)
+      // The fragment ring alternates the block's two halves (the f16 hi fragments
+      // of k-steps 2kb, 2kb+1; the 32-byte fp8 fragment), 8 cycle units each: the
+      // same 2 x 8 VGPRs in flight as the 3-product ring (b_pipeline<KS, 2>)
+      const char* w8 = (const char*)(wt + wlo);
+      auto ld_h = [&](int kb) { return F2{frag_ld(wt, ns, 2 * kb, KS, lane), frag_ld(wt, ns, 2 * kb + 1, KS, lane)}; };
+      auto ld_f = [&](int kb) {
+        const uint4* f = (const uint4*)(w8 + ((size_t)(ns * (KS / 2) + kb) * 64 + lane) * 32);
+        return F2{f[0], f[1]};
+      };
+      F2 rh = ld_h(0), rf = ld_f(0);
+#pragma unroll 1
+      for (int kb = 0; kb < KS / 2; ++kb) {
+        const int kn = min(kb + 1, KS / 2 - 1);
 #pragma unroll
-      for (int jt = 0; jt < VT; ++jt) {
-        const int off = kimg<V>(jt * 32 + l32, 2 * ks + hh);
-        const frag ah = lds_frag(m_hi, off);
-        const frag al = SPLIT ? lds_frag(m_lo, off) : ah;
-        mma<PREC>(adh[jt], ah, al, w.a, w.b);
+        for (int jt = 0; jt < VT; ++jt) {
+          const int row = jt * 32 + l32;
+          adh[jt] = mfma<true>(lds_frag(m_hi, kimg<V>(row, 4 * kb + hh)), rh.a, adh[jt]);
+          adh[jt] = mfma<true>(lds_frag(m_hi, kimg<V>(row, 4 * kb + 2 + hh)), rh.b, adh[jt]);
+        }
+        rh = ld_h(kn);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jt = 0; jt < VT; ++jt) {
+          const int row = jt * 32 + l32;
+          const uint4 p0 = ld16(m_lo + kimg<V>(row, 4 * kb + 2 * hh)), p1 = ld16(m_lo + kimg<V>(row, 4 * kb + 2 * hh + 1));
+          adh[jt] = mfma_f8corr(p0, p1, rf.a, rf.b, adh[jt]);
+        }
+        rf = ld_f(kn);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    };
-    b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)
+    } else {
+      auto ldb = [&](int ks) { return F2{frag_ld(wt, ns, ks, KS, lane), frag{}}; };
+      auto pb = [&](int ks, const F2& w) {
+#pragma unroll
+        for (int jt = 0; jt < VT; ++jt) {
+          const frag ah = lds_frag(m_hi, kimg<V>(jt * 32 + l32, 2 * ks + hh));
+          mma<PREC>(adh[jt], ah, ah, w.a, w.b);
+        }
+      };
+      b_pipeline<KS, 2, 1>(ldb, pb);  // rolled ring: measured 3.5 % over b_direct / full unroll (spills)
+    }
     // dM_c^T -> HBM [c][n][N] (weight-gradient operand).  Issued after the last
     // weight-fragment wait of the channel: vmcnt is in order, so a store ahead of
     // a load would make that load's wait cover the store too.  The stores then

@@ -74,11 +74,19 @@ def test_two_rank_engine_step_equals_full_batch(tmp_path, shape):
     # the all-reduced gradients equal the full batch's up to rounding: the
     # summation order differs, and each rank picks its backward's power-of-two
     # gradient scale from its own max |dL/dh_T| (ggnn_common.h gscale), so the
-    # f16 limb roundings differ (the mode's own error vs float64 is <= 1e-3)
-    for s in range(2):
+    # roundings at the bottom of the f16 / e5m2 ranges differ (the mode's own
+    # error vs float64 is <= 1e-3).  Step 0 (same weights) is the equivalence
+    # itself: measured 1.5-1.7e-7.  Step 1 starts from weights that one Adam
+    # step already moved apart (elements whose gradient is at rounding level
+    # move by ~lr either way, _adam_agreement): measured 4.7-6.7e-5 before
+    # round 6's fp8 limb corrections in the backward, 0.7-1.6e-4 with them
+    # (their rounding is relative to a block's magnitude, so small gradient
+    # elements carry more of it).
+    for s, bar in ((0, 1e-5), (1, 3e-4)):
         ref = d["full_grads"][s]
         err = np.abs(d["dp_grads"][s] - ref).max() / np.abs(ref).max()
-        assert err <= 1e-4, (s, err)
+        print("step %d: dp vs full gradients, max |diff| / max |full| = %.3g" % (s, err))
+        assert err <= bar, (s, err)
     # and so do the weights after two clip + Adam steps at the reference's
     # epsilon 1e-8 (chem_tensorflow.py:494)
     step_dp = d["dp_params"] - d["init"]

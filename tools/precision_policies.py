@@ -50,7 +50,8 @@ def table(A, h0, w, Ts):
 
 
 BWD_POLICIES = [("f16x2", "f16x2", "f16x2", "f16"), ("f16x2", "f16", "f16x2", "f16"), ("f16x2", "f16x2", "f16", "f16"),
-                ("f16x2", "f16", "f16", "f16"), ("f16", "f16x2", "f16x2", "f16")]
+                ("f16x2", "f16", "f16", "f16"), ("f16", "f16x2", "f16x2", "f16"),
+                ("f16x2", "f16", "f8corr", "f16")]  # round 6: k_prop_bwd's corrections on the fp8 MFMA
 
 
 def backward_table(A, h0, w, T, seed=14):
