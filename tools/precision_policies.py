@@ -51,7 +51,8 @@ def table(A, h0, w, Ts):
 
 BWD_POLICIES = [("f16x2", "f16x2", "f16x2", "f16"), ("f16x2", "f16", "f16x2", "f16"), ("f16x2", "f16x2", "f16", "f16"),
                 ("f16x2", "f16", "f16", "f16"), ("f16", "f16x2", "f16x2", "f16"),
-                ("f16x2", "f16", "f8corr", "f16")]  # round 6: k_prop_bwd's corrections on the fp8 MFMA
+                ("f16x2", "f16", "f8corr", "f16"),  # round 6: k_prop_bwd's corrections on the fp8 MFMA
+                ("f16x2", "f8lo", "f8corr", "f16")]  # round 6, shipped: + k_gru_bwd's f16 dz with W's lo on fp8
 
 
 def backward_table(A, h0, w, T, seed=14):
@@ -79,7 +80,8 @@ def main_backward(b):
                    "dzg, dM operands of the dh / dX chain; gru_wt = Wc^T, Wg^T in k_gru_bwd's products; prop_wt = "
                    "W_c^T in k_prop_bwd's dM W_c^T; wgrad = both operands of the weight-gradient products. Forward "
                    "caches exact, accumulation float64; value = max over the seven gradients of max |err| / "
-                   "max |ref| (the fp32 bar is 1e-3). Round 5 ships gru_wt=f16, prop_wt=f16 (hi weight limbs in k_gru_bwd and k_prop_bwd).",
+                   "max |ref| (the fp32 bar is 1e-3). Round 5 shipped gru_wt=f16, prop_wt=f16 (hi weight limbs in k_gru_bwd and k_prop_bwd); "
+                   "round 6 ships gru_wt=f8lo (f16 dz x f16 W + e5m2 dz x e4m3 W_lo), prop_wt=f8corr (both limb corrections on the fp8 MFMA).",
            "configs[2]_synthetic": {"shape": "b=%d v=128 hidden=256 C=8 T=5, SURVEY §8d seed 1" % b,
                                     "policies": backward_table(A, h0, w, 5)}}
     At = trees(b, 30, 46, 3)
@@ -87,7 +89,7 @@ def main_backward(b):
     wt = O.synthetic_weights(256, 92, seed=3, parity_bias=False)
     res["dependency_trees"] = {"shape": "b=%d v=30 hidden=256 E=46 (C=92) T=5, Zipf labels" % b,
                                "policies": backward_table(At, h0t, wt, 5)}
-    with open(os.path.join(ROOT, "profiles", "r05_backward_policies.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", "r06_backward_policies.json"), "w") as f:
         json.dump(res, f, indent=1)
 
 
