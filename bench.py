@@ -67,6 +67,10 @@ def kernel_issued_flops(kind, b, v, h, C, T, precision):
     where the adjacency (exact 0/1) is one side (AGG), 1 for the weight
     gradients (single-limb operands); prop_bwd adds its dbeta product
     (dX^T . deg: one 32-column MFMA tile per channel over K = v, 2 limbs).
+    Round 6: the backward's limb corrections run on the block-scaled fp8 MFMA,
+    counted here in f16-equivalent cycles (one v_mfma_scale_f32_32x32x64 fp8 =
+    two 32x32x16 f16): prop_bwd's dM W_c^T = hi x hi + both corrections = 2
+    products, gru_bwd's dz W^T = hi x hi + e5m2 dz x e4m3 W_lo = 1.5 products.
     16-bit modes issue the algorithmic count."""
     f = flops_per_graph(v, h, C, T)
     if precision != "fp32":
@@ -77,11 +81,11 @@ def kernel_issued_flops(kind, b, v, h, C, T, precision):
     if kind == "prop_fwd":
         return b * (3 * f["mt"] + 2 * f["agg"])
     if kind == "prop_bwd":
-        return b * (3 * f["mt"] + 2 * f["agg"] + dbeta)
+        return b * (2 * f["mt"] + 2 * f["agg"] + dbeta)
     if kind == "gru_fwd":
         return 3 * b * f["gru"]
-    if kind == "gru_bwd":   # dz hi/lo x the weights' hi limb only (round 5): 2 products
-        return 2 * b * f["gru"]
+    if kind == "gru_bwd":   # f16 dz x f16 W + e5m2 dz x e4m3 W_lo (round 6): 1.5 products
+        return 3 * b * f["gru"] // 2
     return kernel_algo_flops(kind, b, v, h, C, T)
 
 

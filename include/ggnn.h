@@ -69,7 +69,10 @@ enum {
  *   GGNN_FP32_PARITY  every non-exact operand carried as an f16 hi/lo limb
  *                     pair (3 MFMAs per product, ~22-bit operand mantissa),
  *                     fp32 activations: matches the reference's fp32
- *                     arithmetic to <= 1e-3 (tests/test_gpu_parity.py) */
+ *                     arithmetic to <= 1e-3 (tests/test_gpu_parity.py).  The
+ *                     backward's dz W^T / dM W_c^T products run their limb
+ *                     corrections on the block-scaled fp8 MFMA (e5m2 x e4m3;
+ *                     DESIGN.md §8.5); the forward keeps three f16 MFMAs */
 #define GGNN_FP32_PARITY 2
 #define GGNN_FP16 4
 /* Empty-channel skipping.  The staged adjacency carries a
@@ -149,7 +152,9 @@ int ggnn_weight_pack_bytes(const ggnn_dims* d, size_t* bytes);
 
 /* Convert fp32 master weights into the engine's MFMA fragment layouts, in the
  * precision policy of d->flags: bf16 (flag 0), f16 (GGNN_FP16) or an f16
- * hi/lo limb pair per element (GGNN_FP32_PARITY); plus the fp32 bias copies
+ * hi/lo limb pair per element (GGNN_FP32_PARITY; the backward's transposed
+ * packs carry e4m3 correction fragments in place of the lo limbs, clamped to
+ * +-448 after their power-of-two scaling); plus the fp32 bias copies
  * and the general path's fp32 weight copies (one per timestep under edge
  * dropout, masked).  edge_biases may be NULL when !(flags & GGNN_USE_EDGE_BIAS). */
 int ggnn_pack_weights(const ggnn_dims* d, void* pack,
