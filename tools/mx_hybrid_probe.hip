@@ -249,6 +249,36 @@ static int part1() {
   return amb + bad[0] + bad[1];
 }
 
+// ---------------------------------------------------------------- part 1b
+// byte order of the packed converts the kernels use (ggnn_common.h pk4_bf8,
+// pk4_fp8, f16x8_to_fp8): element i of the source -> byte i of the result
+typedef short v2i16_t __attribute__((ext_vector_type(2)));
+typedef _Float16 v2f16_t __attribute__((ext_vector_type(2)));
+__global__ void k_cvt_order(unsigned* o) {
+  unsigned w = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(1.0f, 2.0f, 0, false);
+  o[0] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(3.0f, 4.0f, (int)w, true);
+  w = (unsigned)__builtin_amdgcn_cvt_pk_bf8_f32(1.0f, 2.0f, 0, false);
+  o[1] = (unsigned)__builtin_amdgcn_cvt_pk_bf8_f32(3.0f, 4.0f, (int)w, true);
+  v2i16_t r = {0, 0};
+  const v2f16_t a = {(_Float16)1.0f, (_Float16)2.0f}, b = {(_Float16)3.0f, (_Float16)4.0f};
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, a, 1.0f, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, b, 1.0f, true);
+  o[2] = __builtin_bit_cast(unsigned, r);
+}
+static int part1b() {
+  unsigned* d;
+  CHK(hipMalloc(&d, 16));
+  hipLaunchKernelGGL(k_cvt_order, dim3(1), dim3(1), 0, 0, d);
+  unsigned h[3];
+  CHK(hipMemcpy(h, d, 12, hipMemcpyDeviceToHost));
+  // e4m3 1,2,3,4 = 0x38 0x40 0x44 0x48; e5m2 1,2,3,4 = 0x3C 0x40 0x42 0x44
+  const bool ok = h[0] == 0x48444038u && h[1] == 0x4442403Cu && h[2] == 0x48444038u;
+  printf("{\"part\": \"cvt_order\", \"fp8_f32\": \"0x%08x\", \"bf8_f32\": \"0x%08x\", \"fp8_f16\": \"0x%08x\", "
+         "\"element_i_to_byte_i\": %s}\n", h[0], h[1], h[2], ok ? "true" : "false");
+  fflush(stdout);
+  return ok ? 0 : 1;
+}
+
 // ---------------------------------------------------------------- part 2
 constexpr int R = 128, K = 256, NT = 512, NITER = 64;
 constexpr int IMG = R * K * 2;  // one f16 limb image, bytes (= the fp8 [hi | lo] image)
@@ -347,7 +377,8 @@ static u16 f2h(float x) {
 int main(int argc, char** argv) {
   const double secs = argc > 1 ? atof(argv[1]) : 3.0;
   const int rounds = argc > 2 ? atoi(argv[2]) : 2;
-  const int p1 = part1();
+  if (argc > 3 && argv[3][0] == 'c') return part1b();
+  const int p1 = part1() + part1b();
   if (argc > 3) return p1;
   const int NWG = 256;
   std::vector<u16> ah(R * K), al(R * K), bh(K * K), bl(K * K);
